@@ -1,0 +1,151 @@
+/*
+ * lievae.h — C ABI of liblievae_hip.so, the MI355X (gfx950) kernels behind the
+ * drop-in `lie_vae` Python API (SO(3) latent hot path of pimdh/lie-vae).
+ *
+ * The reference has no FFI: its "operator API" is the Python functions of
+ * lie_vae/lie_tools.py, the modules of lie_vae/reparameterize.py and
+ * lie_vae/decoders.py.  Each entry point below names the reference symbol
+ * (file:line under the reference root) it replaces.  The ctypes binding that
+ * calls them is lie-vae_amd/lie_vae/_lib.py.
+ *
+ * Conventions
+ *  - All tensor arguments are device pointers to contiguous row-major arrays,
+ *    allocated and owned by the caller.  The library never allocates device
+ *    memory; backward passes that need scratch take a caller workspace sized
+ *    by the matching *_workspace() query.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Calls
+ *    are asynchronous on that stream and never synchronise the host, so they
+ *    are safe to capture in a hipGraph.
+ *  - Return 0 (LV_OK) or a negative LV_ERR_* code; lv_last_error() returns a
+ *    thread-local message for the last failing call on this thread.
+ *  - n == 0 is a valid no-op.
+ *  - Rotation matrices are (n,3,3); quaternions are scalar-LAST (x,y,z,w) as in
+ *    the reference; Euler angles are ZYZ (alpha, beta, gamma).
+ */
+#ifndef LIEVAE_H_
+#define LIEVAE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LV_OK 0
+#define LV_ERR_ARG (-1)         /* bad shape / pointer / unsupported size */
+#define LV_ERR_HIP (-2)         /* HIP runtime error (launch failure)      */
+#define LV_ERR_WORKSPACE (-3)   /* workspace too small                    */
+
+#define LV_DTYPE_F32 0
+#define LV_DTYPE_BF16 1
+
+#define LV_MAX_DEGREE 20        /* largest l_max compiled in              */
+#define LV_MAX_CHANNELS 64      /* largest rep_copies C per call          */
+
+int lv_abi_version(void);
+const char* lv_last_error(void);
+int lv_max_degree(void);
+
+/* ---- so(3) exponential: lie_tools.py:56-64 `rodrigues` (a1+a2) --------------
+ * v (n,3) -> R (n,3,3).  No small-angle branch: |v| == 0 gives NaN like the
+ * reference. */
+int lv_so3_exp_fwd(const float* v, float* R, int64_t n, void* stream);
+int lv_so3_exp_bwd(const float* v, const float* gR, float* gv, int64_t n, void* stream);
+
+/* ---- SO3reparameterize.nsample: reparameterize.py:269-273 --------------------
+ * z[s,b] = mu[b] @ rodrigues(v[s,b]);  v (ns,B,3), mu (B,3,3), z (ns,B,3,3).
+ * Backward sums gmu over the ns samples in a fixed order (deterministic). */
+int lv_so3_sample_fwd(const float* mu, const float* v, float* z, int64_t ns, int64_t B,
+                      void* stream);
+int lv_so3_sample_bwd(const float* mu, const float* v, const float* gz, float* gmu, float* gv,
+                      int64_t ns, int64_t B, void* stream);
+
+/* ---- quaternions_to_group_matrix: lie_tools.py:183-192 (a3) ---------------- */
+int lv_quat_to_mat_fwd(const float* q, float* R, int64_t n, void* stream);
+int lv_quat_to_mat_bwd(const float* q, const float* gR, float* gq, int64_t n, void* stream);
+
+/* ---- group_matrix_to_quaternions: lie_tools.py:112-157 (a4) -----------------
+ * Mirrors the 1e-6 epsilon and the argmax case choice (gradient flows through
+ * the chosen case only). */
+int lv_mat_to_quat_fwd(const float* R, float* q, int64_t n, void* stream);
+int lv_mat_to_quat_bwd(const float* R, const float* gq, float* gR, int64_t n, void* stream);
+
+/* ---- quaternions_to_eazyz: lie_tools.py:160-175 (a5) ----------------------- */
+int lv_quat_to_eazyz_fwd(const float* q, float* ang, int64_t n, void* stream);
+int lv_quat_to_eazyz_bwd(const float* q, const float* gang, float* gq, int64_t n, void* stream);
+
+/* ---- group_matrix_to_eazyz: lie_tools.py:178-180 (a6 = a4 then a5) --------- */
+int lv_mat_to_eazyz_fwd(const float* R, float* ang, int64_t n, void* stream);
+int lv_mat_to_eazyz_bwd(const float* R, const float* gang, float* gR, int64_t n, void* stream);
+
+/* ---- s2s1rodrigues: lie_tools.py:67-78 (S2S1Mean, reparameterize.py:167-181) */
+int lv_s2s1_fwd(const float* axis, const float* cs, float* R, int64_t n, void* stream);
+int lv_s2s1_bwd(const float* axis, const float* cs, const float* gR, float* gaxis, float* gcs,
+                int64_t n, void* stream);
+
+/* ---- s2s2_gram_schmidt, fp64: lie_tools.py:81-89 (S2S2Mean, reparameterize.py:184-197)
+ * Crosses along the last axis (the reference's torch.cross without dim is
+ * wrong at batch 3; documented deviation). */
+int lv_s2s2_fwd_f64(const double* v1, const double* v2, double* R, int64_t n, void* stream);
+int lv_s2s2_bwd_f64(const double* v1, const double* v2, const double* gR, double* gv1,
+                    double* gv2, int64_t n, void* stream);
+
+/* ---- wigner_d_matrix for l = 0..L, packed: lie_tools.py:211-223 (a9) -------
+ * ang (n,3) -> D (n, sum_l (2l+1)^2), block l row-major at offset
+ * sum_{k<l}(2k+1)^2.  Parity/debug entry point; the hot path never materialises D. */
+int lv_wigner_d_fwd(const float* ang, float* D, int64_t n, int L, void* stream);
+
+/* ---- block_wigner_matrix_multiply: lie_tools.py:226-253 (a10) --------------
+ * out[s, l^2 + i, c] = sum_j D_l(ang[s])[i,j] (or D^T if transpose) F[s, l^2 + j, c]
+ * F is (M, C) shared when F_batch_stride == 0 (ActionNet's expand, decoders.py:53)
+ * or (n, M, C) with F_batch_stride == M*C.  M = (L+1)^2, 1 <= C <= 64.
+ * out (n, M, C) in out_dtype (LV_DTYPE_F32 | LV_DTYPE_BF16); arithmetic is fp32. */
+int lv_group_action_fwd(const float* ang, const float* F, int64_t F_batch_stride, void* out,
+                        int out_dtype, int64_t n, int L, int C, int transpose, void* stream);
+
+/* Backward of lv_group_action_fwd (fp32 gout).  gang (n,3).  gF is (M,C) summed
+ * over the batch (deterministic two-stage reduction through the workspace) when
+ * F_batch_stride == 0, else (n,M,C).  Workspace bytes from the query below. */
+size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F);
+int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride,
+                        const float* gout, float* gang, float* gF, int64_t n, int L, int C,
+                        int transpose, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- fused metric kernel: z = mu @ rodrigues(v) -> ZYZ -> block D(z)·F ------
+ * reparameterize.py:269-273 + vae.py:182 + decoders.py:47-56 in one pass.
+ * mu (n,3,3) or NULL (identity); v (n,3); optional ang_out (n,3) receives the
+ * Euler angles (for the backward).  Other arguments as lv_group_action_fwd. */
+int lv_fused_exp_action_fwd(const float* mu, const float* v, const float* F,
+                            int64_t F_batch_stride, void* out, int out_dtype, float* ang_out,
+                            int64_t n, int L, int C, int transpose, void* stream);
+
+/* ---- N0reparameterize: reparameterize.py:100-145 (a12) ---------------------
+ * sigma = softplus(h) (beta 1, threshold 20), h/sigma (B,3). */
+int lv_softplus_fwd(const float* h, float* sigma, int64_t n, void* stream);
+int lv_softplus_bwd(const float* h, const float* gsigma, float* gh, int64_t n, void* stream);
+/* v[s,b,:] = eps[s,b,:] * sigma[b,:]; backward sums gsigma over s (deterministic). */
+int lv_n0_sample_fwd(const float* sigma, const float* eps, float* v, int64_t ns, int64_t B,
+                     void* stream);
+int lv_n0_sample_bwd(const float* eps, const float* gv, float* gsigma, int64_t ns, int64_t B,
+                     void* stream);
+
+/* ---- SO3reparameterize.log_posterior: reparameterize.py:233-263 (a13+a15) ---
+ * v (ns,B,3), sigma (B,3) -> out (ns,B): logsumexp over the 2k+1 wrapped terms. */
+int lv_so3_log_posterior_fwd(const float* v, const float* sigma, float* out, int64_t ns,
+                             int64_t B, int k, void* stream);
+int lv_so3_log_posterior_bwd(const float* v, const float* sigma, const float* gout, float* gv,
+                             float* gsigma, int64_t ns, int64_t B, int k, void* stream);
+
+/* ---- timing helper for bench.py: K back-to-back launches of the fused kernel
+ * from C, so the host-side launch cost is not Python's.  Same arguments as
+ * lv_fused_exp_action_fwd plus the repeat count. */
+int lv_fused_exp_action_fwd_repeat(const float* mu, const float* v, const float* F,
+                                   int64_t F_batch_stride, void* out, int out_dtype,
+                                   float* ang_out, int64_t n, int L, int C, int transpose,
+                                   int repeats, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIEVAE_H_ */

@@ -1,0 +1,143 @@
+// The per-degree factored Wigner chain shared by the forward and backward kernels.
+//
+// The reference evaluates D_l = X(a)·J·X(b)·J·X(c) as four dense bmm's per degree and
+// then D_l·F (lie_tools.py:211-253).  Here one lane owns one column c of one sample's
+// spectrum block and applies the factors right-to-left to that column, never forming D:
+//
+//   y = X(a) · J · X(b) · J · X(c) · F[:, c]
+//
+// X(θ) has two non-zeros per row (cos on the diagonal, sin on the anti-diagonal,
+// frequency l-i for row i, lie_tools.py:195-208) and J_l is a compile-time constant
+// table (~1/4 dense), so each product is a short chain of register FMAs with literal
+// coefficients: ~2·nnz(J_l) + 6(2l+1) FLOP-pairs per column instead of the reference's
+// 8(2l+1)^3 + 2(2l+1)^2·C per sample.
+#pragma once
+#include "j_tables.h"
+#include "lv_common.h"
+
+#define LV_CV(x) decltype(x)::value
+
+namespace lv {
+
+// cos/sin of f·angle for the three Euler slots (0 = a, 1 = b, 2 = c), f = 0..LT.
+template <int LT>
+struct TrigTab {
+  float c[3][LT + 1];
+  float s[3][LT + 1];
+};
+
+// Fill multiples by the rotation recurrence from exact (cos, sin) of each angle.
+// Error grows ~f·ulp: at f = 20 it is below the reference's own fp32 sin(f·θ) error.
+template <int LT>
+__device__ __forceinline__ void trig_fill(TrigTab<LT>& t, const float c1[3], const float s1[3],
+                                          int upto) {
+  sfor<3>([&](auto A) {
+    constexpr int a = LV_CV(A);
+    t.c[a][0] = 1.f;
+    t.s[a][0] = 0.f;
+    if constexpr (LT >= 1) {
+      t.c[a][1] = c1[a];
+      t.s[a][1] = s1[a];
+    }
+    sfor<LT + 1>([&](auto F) {
+      constexpr int f = LV_CV(F);
+      if constexpr (f >= 2) {
+        if (f <= upto) {
+          t.c[a][f] = fmaf(t.c[a][f - 1], c1[a], -(t.s[a][f - 1] * s1[a]));
+          t.s[a][f] = fmaf(t.s[a][f - 1], c1[a], t.c[a][f - 1] * s1[a]);
+        }
+      }
+    });
+  });
+}
+
+// y = X_l(θ_A) x      (row i: cos(fθ) x_i + sin(fθ) x_{2l-i}, f = l - i)
+template <int l, int A, int LT>
+__device__ __forceinline__ void xrot(const TrigTab<LT>& t, const float (&x)[2 * l + 1],
+                                     float (&y)[2 * l + 1]) {
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) {
+      y[i] = x[i];
+    } else if constexpr (f > 0) {
+      y[i] = fmaf(t.c[A][f], x[i], t.s[A][f] * x[2 * l - i]);
+    } else {
+      y[i] = fmaf(t.c[A][-f], x[i], -(t.s[A][-f] * x[2 * l - i]));
+    }
+  });
+}
+
+// y = X_l(θ_A)^T x = X_l(-θ_A) x
+template <int l, int A, int LT>
+__device__ __forceinline__ void xrot_t(const TrigTab<LT>& t, const float (&x)[2 * l + 1],
+                                       float (&y)[2 * l + 1]) {
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) {
+      y[i] = x[i];
+    } else if constexpr (f > 0) {
+      y[i] = fmaf(t.c[A][f], x[i], -(t.s[A][f] * x[2 * l - i]));
+    } else {
+      y[i] = fmaf(t.c[A][-f], x[i], t.s[A][-f] * x[2 * l - i]);
+    }
+  });
+}
+
+// <g, dX_l(θ_A)/dθ · x>: row i of dX/dθ is (-f sin(fθ) at i, f cos(fθ) at 2l-i).
+template <int l, int A, int LT>
+__device__ __forceinline__ float xrot_dot_deriv(const TrigTab<LT>& t, const float (&g)[2 * l + 1],
+                                                const float (&x)[2 * l + 1]) {
+  float acc = 0.f;
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f > 0) {
+      const float d = fmaf(-t.s[A][f], x[i], t.c[A][f] * x[2 * l - i]);
+      acc = fmaf(g[i], (float)f * d, acc);
+    } else if constexpr (f < 0) {
+      // sin(fθ) = -sin(|f|θ), cos(fθ) = cos(|f|θ)
+      const float d = fmaf(t.s[A][-f], x[i], t.c[A][-f] * x[2 * l - i]);
+      acc = fmaf(g[i], (float)f * d, acc);
+    }
+  });
+  return acc;
+}
+
+// y = J_l x with J_l's non-zeros as literal coefficients (J is symmetric: J^T = J).
+template <int l>
+__device__ __forceinline__ void jmul(const float (&x)[2 * l + 1], float (&y)[2 * l + 1]) {
+  constexpr int n = 2 * l + 1;
+  constexpr const float* J = lv_j::jtab<l>();
+  sfor<n>([&](auto P) {
+    constexpr int p = LV_CV(P);
+    float acc = 0.f;
+    sfor<n>([&](auto K) {
+      constexpr int k = LV_CV(K);
+      constexpr float v = J[p * n + k];
+      if constexpr (v != 0.f) acc = fmaf(v, x[k], acc);
+    });
+    y[p] = acc;
+  });
+}
+
+// Number of structural non-zeros of J_l (host-side cost model).
+template <int l>
+constexpr int j_nnz() {
+  constexpr int n = 2 * l + 1;
+  constexpr const float* J = lv_j::jtab<l>();
+  int c = 0;
+  for (int i = 0; i < n * n; ++i) c += (J[i] != 0.f);
+  return c;
+}
+
+// Make this wave's LDS writes visible to its own later reads (and keep the compiler
+// from moving LDS traffic across the point).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+}  // namespace lv

@@ -1,0 +1,55 @@
+// Common plumbing for the lie-vae MI355X kernels: error state, dtype tags,
+// compile-time loops.  gfx950 only; no CUDA/HIP dual paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <utility>
+
+#include "../../include/lievae.h"
+
+namespace lv {
+
+// Thread-local last-error text (lv_last_error()).
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define LV_CHECK_ARG(cond, ...)                      \
+  do {                                               \
+    if (!(cond)) {                                   \
+      ::lv::set_error(__VA_ARGS__);                  \
+      return LV_ERR_ARG;                             \
+    }                                                \
+  } while (0)
+
+#define LV_RETURN_LAUNCH(kname)                                               \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess) {                                                   \
+      ::lv::set_error("%s: launch failed: %s", kname, hipGetErrorString(e_)); \
+      return LV_ERR_HIP;                                                      \
+    }                                                                         \
+    return LV_OK;                                                             \
+  } while (0)
+
+// ---------------------------------------------------------------- static_for
+template <class F, int... Is>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------- out types
+__device__ __forceinline__ void store_out(float* p, float v) { *p = v; }
+__device__ __forceinline__ void store_out(__hip_bfloat16* p, float v) { *p = __float2bfloat16(v); }
+__device__ __forceinline__ float load_in(const float* p) { return *p; }
+__device__ __forceinline__ float load_in(const __hip_bfloat16* p) { return __bfloat162float(*p); }
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace lv

@@ -1,0 +1,111 @@
+"""ctypes binding of liblievae_hip.so (C ABI declared in include/lievae.h).
+
+The library is built in-tree by ``make -C lie-vae_amd/csrc`` (or
+``__graft_entry__.build()``).  There is no fallback: if the shared object is missing
+or a call fails, this module raises.  Every entry point takes device pointers and the
+caller's current HIP stream, so calls are asynchronous and graph-capturable.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LIEVAE_HIP_LIB", os.path.join(_HERE, "liblievae_hip.so"))
+
+LV_DTYPE_F32 = 0
+LV_DTYPE_BF16 = 1
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_SZ = ctypes.c_size_t
+
+# name -> argtypes (restype int unless noted)
+_SIGS = {
+    "lv_abi_version": [],
+    "lv_max_degree": [],
+    "lv_so3_exp_fwd": [_P, _P, _I64, _P],
+    "lv_so3_exp_bwd": [_P, _P, _P, _I64, _P],
+    "lv_so3_sample_fwd": [_P, _P, _P, _I64, _I64, _P],
+    "lv_so3_sample_bwd": [_P, _P, _P, _P, _P, _I64, _I64, _P],
+    "lv_quat_to_mat_fwd": [_P, _P, _I64, _P],
+    "lv_quat_to_mat_bwd": [_P, _P, _P, _I64, _P],
+    "lv_mat_to_quat_fwd": [_P, _P, _I64, _P],
+    "lv_mat_to_quat_bwd": [_P, _P, _P, _I64, _P],
+    "lv_quat_to_eazyz_fwd": [_P, _P, _I64, _P],
+    "lv_quat_to_eazyz_bwd": [_P, _P, _P, _I64, _P],
+    "lv_mat_to_eazyz_fwd": [_P, _P, _I64, _P],
+    "lv_mat_to_eazyz_bwd": [_P, _P, _P, _I64, _P],
+    "lv_s2s1_fwd": [_P, _P, _P, _I64, _P],
+    "lv_s2s1_bwd": [_P, _P, _P, _P, _P, _I64, _P],
+    "lv_s2s2_fwd_f64": [_P, _P, _P, _I64, _P],
+    "lv_s2s2_bwd_f64": [_P, _P, _P, _P, _P, _I64, _P],
+    "lv_wigner_d_fwd": [_P, _P, _I64, _I, _P],
+    "lv_group_action_fwd": [_P, _P, _I64, _P, _I, _I64, _I, _I, _I, _P],
+    "lv_group_action_bwd": [_P, _P, _I64, _P, _P, _P, _I64, _I, _I, _I, _P, _SZ, _P],
+    "lv_fused_exp_action_fwd": [_P, _P, _P, _I64, _P, _I, _P, _I64, _I, _I, _I, _P],
+    "lv_fused_exp_action_fwd_repeat": [_P, _P, _P, _I64, _P, _I, _P, _I64, _I, _I, _I, _I, _P],
+    "lv_softplus_fwd": [_P, _P, _I64, _P],
+    "lv_softplus_bwd": [_P, _P, _P, _I64, _P],
+    "lv_n0_sample_fwd": [_P, _P, _P, _I64, _I64, _P],
+    "lv_n0_sample_bwd": [_P, _P, _P, _I64, _I64, _P],
+    "lv_so3_log_posterior_fwd": [_P, _P, _P, _I64, _I64, _I, _P],
+    "lv_so3_log_posterior_bwd": [_P, _P, _P, _P, _P, _I64, _I64, _I, _P],
+}
+_RESTYPES = {"lv_group_action_bwd_workspace": _SZ, "lv_last_error": ctypes.c_char_p}
+_SIGS_EXTRA = {"lv_group_action_bwd_workspace": [_I64, _I, _I, _I], "lv_last_error": []}
+
+EXPORTED = sorted(list(_SIGS) + list(_SIGS_EXTRA))
+
+_lib = None
+
+
+class LieVaeHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the shared library; raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"lie_vae: HIP library not found at {LIB_PATH}; build it with "
+            "`make -C lie-vae_amd/csrc` (or __graft_entry__.build()). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in {**_SIGS, **_SIGS_EXTRA}.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def last_error():
+    return load().lv_last_error().decode(errors="replace")
+
+
+def call(name, *args):
+    """Invoke an entry point; non-zero return -> LieVaeHipError with the library message."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise LieVaeHipError(f"{name} failed ({rc}): {last_error()}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def require_device(*tensors):
+    """The HIP path only: refuse CPU tensors loudly instead of silently falling back."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "lie_vae ops run only on the MI355X HIP path (got a CPU tensor); "
+                "move inputs to a cuda:N (HIP) device. There is no CPU fallback.")

@@ -1,0 +1,296 @@
+"""torch.autograd.Functions over the C ABI.  Forward and backward both run the HIP
+kernels of liblievae_hip.so on the caller's current stream; nothing here computes on
+the CPU.  Inputs are made contiguous fp32 (fp64 for the S2S2 Gram–Schmidt, as in the
+reference, ``reparameterize.py:195-197``)."""
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+
+F32 = torch.float32
+
+
+def _prep(t, dtype=F32):
+    _lib.require_device(t)
+    return t.contiguous() if t.dtype == dtype else t.to(dtype).contiguous()
+
+
+def _empty(shape, like, dtype=F32):
+    return torch.empty(shape, device=like.device, dtype=dtype)
+
+
+def _flat(t, last):
+    """View (..., *last) as (n, *last); returns the batch shape too."""
+    lead = t.shape[: t.dim() - len(last)]
+    n = 1
+    for d in lead:
+        n *= d
+    return t.reshape(n, *last), lead, n
+
+
+# ------------------------------------------------------------- unary maps
+class _Unary(torch.autograd.Function):
+    """Generic per-sample map x (n, *IN) -> y (n, *OUT) with a VJP kernel."""
+
+    @staticmethod
+    def forward(ctx, x, spec):
+        fwd, bwd, ishape, oshape = spec
+        xf, lead, n = _flat(_prep(x), ishape)
+        y = _empty((n, *oshape), xf)
+        call(fwd, ptr(xf), ptr(y), n, stream())
+        ctx.save_for_backward(xf)
+        ctx.spec, ctx.lead, ctx.n = spec, lead, n
+        return y.reshape(*lead, *oshape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (xf,) = ctx.saved_tensors
+        fwd, bwd, ishape, oshape = ctx.spec
+        gyf = _prep(gy).reshape(ctx.n, *oshape)
+        gx = _empty((ctx.n, *ishape), xf)
+        call(bwd, ptr(xf), ptr(gyf), ptr(gx), ctx.n, stream())
+        return gx.reshape(*ctx.lead, *ishape), None
+
+
+SO3_EXP = ("lv_so3_exp_fwd", "lv_so3_exp_bwd", (3,), (3, 3))
+QUAT_TO_MAT = ("lv_quat_to_mat_fwd", "lv_quat_to_mat_bwd", (4,), (3, 3))
+MAT_TO_QUAT = ("lv_mat_to_quat_fwd", "lv_mat_to_quat_bwd", (3, 3), (4,))
+QUAT_TO_EAZYZ = ("lv_quat_to_eazyz_fwd", "lv_quat_to_eazyz_bwd", (4,), (3,))
+MAT_TO_EAZYZ = ("lv_mat_to_eazyz_fwd", "lv_mat_to_eazyz_bwd", (3, 3), (3,))
+SOFTPLUS = ("lv_softplus_fwd", "lv_softplus_bwd", (), ())
+
+
+def unary(x, spec):
+    return _Unary.apply(x, spec)
+
+
+# ----------------------------------------------------------- binary maps
+class _S2S1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, axis, cs):
+        a, lead, n = _flat(_prep(axis), (3,))
+        c, _, _ = _flat(_prep(cs), (2,))
+        r = _empty((n, 3, 3), a)
+        call("lv_s2s1_fwd", ptr(a), ptr(c), ptr(r), n, stream())
+        ctx.save_for_backward(a, c)
+        ctx.lead, ctx.n = lead, n
+        return r.reshape(*lead, 3, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, c = ctx.saved_tensors
+        gf = _prep(g).reshape(ctx.n, 3, 3)
+        ga, gc = _empty((ctx.n, 3), a), _empty((ctx.n, 2), a)
+        call("lv_s2s1_bwd", ptr(a), ptr(c), ptr(gf), ptr(ga), ptr(gc), ctx.n, stream())
+        return ga.reshape(*ctx.lead, 3), gc.reshape(*ctx.lead, 2)
+
+
+class _S2S2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v1, v2):
+        f64 = torch.float64
+        a, lead, n = _flat(_prep(v1, f64), (3,))
+        b, _, _ = _flat(_prep(v2, f64), (3,))
+        r = _empty((n, 3, 3), a, f64)
+        call("lv_s2s2_fwd_f64", ptr(a), ptr(b), ptr(r), n, stream())
+        ctx.save_for_backward(a, b)
+        ctx.lead, ctx.n = lead, n
+        return r.reshape(*lead, 3, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        gf = _prep(g, torch.float64).reshape(ctx.n, 3, 3)
+        g1, g2 = torch.empty_like(a), torch.empty_like(b)
+        call("lv_s2s2_bwd_f64", ptr(a), ptr(b), ptr(gf), ptr(g1), ptr(g2), ctx.n, stream())
+        return g1.reshape(*ctx.lead, 3), g2.reshape(*ctx.lead, 3)
+
+
+class _SO3Sample(torch.autograd.Function):
+    """z[s, b] = mu[b] @ exp(v[s, b]) — reparameterize.py:269-273."""
+
+    @staticmethod
+    def forward(ctx, mu, v):
+        mu = _prep(mu)
+        v = _prep(v)
+        ns, B = v.shape[0], v.shape[1]
+        assert mu.shape == (B, 3, 3) and v.shape == (ns, B, 3)
+        z = _empty((ns, B, 3, 3), v)
+        call("lv_so3_sample_fwd", ptr(mu), ptr(v), ptr(z), ns, B, stream())
+        ctx.save_for_backward(mu, v)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        mu, v = ctx.saved_tensors
+        ns, B = v.shape[0], v.shape[1]
+        gz = _prep(gz)
+        gmu, gv = torch.empty_like(mu), torch.empty_like(v)
+        call("lv_so3_sample_bwd", ptr(mu), ptr(v), ptr(gz), ptr(gmu), ptr(gv), ns, B, stream())
+        return gmu, gv
+
+
+class _N0Sample(torch.autograd.Function):
+    """v[s, b] = eps[s, b] * sigma[b] — reparameterize.py:137-141 (eps given)."""
+
+    @staticmethod
+    def forward(ctx, sigma, eps):
+        sigma = _prep(sigma)
+        eps = _prep(eps)
+        ns, B = eps.shape[0], eps.shape[1]
+        v = torch.empty_like(eps)
+        call("lv_n0_sample_fwd", ptr(sigma), ptr(eps), ptr(v), ns, B, stream())
+        ctx.save_for_backward(eps)
+        return v
+
+    @staticmethod
+    def backward(ctx, gv):
+        (eps,) = ctx.saved_tensors
+        ns, B = eps.shape[0], eps.shape[1]
+        gs = _empty((B, 3), eps)
+        call("lv_n0_sample_bwd", ptr(eps), ptr(_prep(gv)), ptr(gs), ns, B, stream())
+        return gs, None
+
+
+class _SO3LogPosterior(torch.autograd.Function):
+    """log q(exp(v) | sigma), 2k+1 wrapped terms — reparameterize.py:233-263."""
+
+    @staticmethod
+    def forward(ctx, v, sigma, k):
+        v = _prep(v)
+        sigma = _prep(sigma)
+        ns, B = v.shape[0], v.shape[1]
+        out = _empty((ns, B), v)
+        call("lv_so3_log_posterior_fwd", ptr(v), ptr(sigma), ptr(out), ns, B, k, stream())
+        ctx.save_for_backward(v, sigma)
+        ctx.k = k
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        v, sigma = ctx.saved_tensors
+        ns, B = v.shape[0], v.shape[1]
+        gv, gs = torch.empty_like(v), torch.empty_like(sigma)
+        call("lv_so3_log_posterior_bwd", ptr(v), ptr(sigma), ptr(_prep(g)), ptr(gv), ptr(gs),
+             ns, B, ctx.k, stream())
+        return gv, gs, None
+
+
+# ------------------------------------------------------------ group action
+class _GroupAction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, angles, spec, L, transpose, out_dtype):
+        angles = _prep(angles)
+        n = angles.shape[0]
+        M = (L + 1) ** 2
+        C = spec.shape[-1]
+        stride = 0 if spec.dim() == 2 else M * C
+        dt = _lib.LV_DTYPE_BF16 if out_dtype == torch.bfloat16 else _lib.LV_DTYPE_F32
+        out = _empty((n, M, C), angles, out_dtype)
+        call("lv_group_action_fwd", ptr(angles), ptr(spec), stride, ptr(out), dt, n, L, C,
+             int(transpose), stream())
+        ctx.save_for_backward(angles, spec)
+        ctx.L, ctx.transpose, ctx.stride = L, transpose, stride
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        angles, spec = ctx.saved_tensors
+        n, L, C = angles.shape[0], ctx.L, spec.shape[-1]
+        gout = _prep(gout)
+        gang = torch.empty_like(angles)
+        gspec = torch.empty_like(spec)
+        ws_bytes = _lib.load().lv_group_action_bwd_workspace(n, L, C, int(ctx.stride == 0))
+        ws = torch.empty(max(ws_bytes, 1), device=angles.device, dtype=torch.uint8)
+        call("lv_group_action_bwd", ptr(angles), ptr(spec), ctx.stride, ptr(gout), ptr(gang),
+             ptr(gspec), n, L, C, int(ctx.transpose), ptr(ws), ws_bytes, stream())
+        return gang, gspec, None, None, None
+
+
+def group_action(angles, spectrum, L, transpose=False, out_dtype=F32):
+    """block_wigner_matrix_multiply on the HIP path; spectrum (M,C), (n,M,C) or a
+    stride-0 expand of (M,C)."""
+    _lib.require_device(angles, spectrum)
+    n = angles.shape[0]
+    M = (L + 1) ** 2
+    C = spectrum.shape[-1]
+    assert spectrum.shape[-2] == M, f"spectrum rows {spectrum.shape[-2]} != (L+1)^2 = {M}"
+    if spectrum.dim() == 3 and spectrum.stride(0) == 0:
+        # (M,C) passed once; autograd routes dF through select+expand back to item_rep
+        spectrum = spectrum[0]
+    return _GroupAction.apply(angles, _contig(spectrum), L, transpose, out_dtype)
+
+
+def _contig(t):
+    return t.contiguous() if t.dtype == F32 else t.float().contiguous()
+
+
+class _FusedExpAction(torch.autograd.Function):
+    """mu@exp(v) -> ZYZ -> block D·F in one launch; backward through the modular kernels."""
+
+    @staticmethod
+    def forward(ctx, mu, v, spec, L, transpose, out_dtype):
+        v = _prep(v)
+        n = v.shape[0]
+        mu_c = _prep(mu) if mu is not None else None
+        M = (L + 1) ** 2
+        C = spec.shape[-1]
+        stride = 0 if spec.dim() == 2 else M * C
+        dt = _lib.LV_DTYPE_BF16 if out_dtype == torch.bfloat16 else _lib.LV_DTYPE_F32
+        out = _empty((n, M, C), v, out_dtype)
+        ang = _empty((n, 3), v)
+        call("lv_fused_exp_action_fwd", ptr(mu_c), ptr(v), ptr(spec), stride, ptr(out), dt,
+             ptr(ang), n, L, C, int(transpose), stream())
+        ctx.save_for_backward(mu_c if mu_c is not None else v.new_empty(0), v, spec, ang)
+        ctx.has_mu, ctx.L, ctx.transpose, ctx.stride = mu is not None, L, transpose, stride
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        mu, v, spec, ang = ctx.saved_tensors
+        n, L, C = v.shape[0], ctx.L, spec.shape[-1]
+        gout = _prep(gout)
+        gang = torch.empty_like(ang)
+        gspec = torch.empty_like(spec)
+        ws_bytes = _lib.load().lv_group_action_bwd_workspace(n, L, C, int(ctx.stride == 0))
+        ws = torch.empty(max(ws_bytes, 1), device=v.device, dtype=torch.uint8)
+        call("lv_group_action_bwd", ptr(ang), ptr(spec), ctx.stride, ptr(gout), ptr(gang),
+             ptr(gspec), n, L, C, int(ctx.transpose), ptr(ws), ws_bytes, stream())
+        z = _empty((n, 3, 3), v)
+        if ctx.has_mu:
+            call("lv_so3_sample_fwd", ptr(mu), ptr(v), ptr(z), 1, n, stream())
+        else:
+            call("lv_so3_exp_fwd", ptr(v), ptr(z), n, stream())
+        gz = torch.empty_like(z)
+        call("lv_mat_to_eazyz_bwd", ptr(z), ptr(gang), ptr(gz), n, stream())
+        gv = torch.empty_like(v)
+        gmu = None
+        if ctx.has_mu:
+            gmu = torch.empty_like(mu)
+            call("lv_so3_sample_bwd", ptr(mu), ptr(v), ptr(gz), ptr(gmu), ptr(gv), 1, n, stream())
+        else:
+            call("lv_so3_exp_bwd", ptr(v), ptr(gz), ptr(gv), n, stream())
+        return gmu, gv, gspec, None, None, None
+
+
+def fused_exp_action(mu, v, spectrum, L, transpose=False, out_dtype=F32):
+    """(mu (n,3,3) or None, v (n,3), spectrum (M,C) or (n,M,C)) -> (n, M, C)."""
+    _lib.require_device(v, spectrum, mu)
+    return _FusedExpAction.apply(mu, v, _contig(spectrum), L, transpose, out_dtype)
+
+
+def wigner_blocks(angles, L):
+    """Packed D_0..D_L for each angle triple (debug / parity), (n, sum (2l+1)^2)."""
+    angles = _prep(angles)
+    n = angles.shape[0]
+    tot = (L + 1) * (2 * L + 1) * (2 * L + 3) // 3
+    D = _empty((n, tot), angles)
+    call("lv_wigner_d_fwd", ptr(angles), ptr(D), n, L, stream())
+    return D
+
+
+s2s1 = _S2S1.apply
+s2s2 = _S2S2.apply
+so3_sample = _SO3Sample.apply
+n0_sample = _N0Sample.apply
+so3_log_posterior = _SO3LogPosterior.apply

@@ -1,0 +1,312 @@
+"""GPU parity of the HIP path (through the C ABI) against the reference.
+
+Three layers of evidence:
+  1. golden vectors produced by the reference code itself (tests/golden, small sizes);
+  2. the CPU oracle (oracle/lie_ref.py) on identical seeded inputs at larger sizes;
+  3. size-independent properties at full BASELINE sizes (orthogonality, D(b)D(a)=D(ab),
+     linearity in F, transpose = inverse).
+
+Tolerance (north_star: "within 1e-5 rel fp32"): graded per sample, normwise —
+||y_s - ref_s|| <= 1e-5 ||ref_s|| — because the reference's own fp32 output differs from
+its fp64 evaluation elementwise by O(1) relative near zeros.  For
+l >= 10 we also require err(HIP vs fp64) <= 2 err(reference fp32 vs fp64).
+"""
+import glob
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def dev(x, device, dtype=None):
+    t = torch.as_tensor(np.asarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(device)
+
+
+def normwise(y, ref):
+    y = np.asarray(y, dtype=np.float64).reshape(len(ref), -1)
+    r = np.asarray(ref, dtype=np.float64).reshape(len(ref), -1)
+    return np.linalg.norm(y - r, axis=1) / np.maximum(np.linalg.norm(r, axis=1), 1e-30)
+
+
+def assert_normwise(y, ref, tol=TOL, what=""):
+    e = normwise(y, ref)
+    assert np.isfinite(e).all(), what
+    assert e.max() <= tol, f"{what}: max per-sample rel err {e.max():.3e} > {tol:.1e}"
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def grad_run(fn, inputs, gout, device, dtypes=None):
+    xs = [dev(x, device, None if dtypes is None else dtypes[i]).requires_grad_(True)
+          for i, x in enumerate(inputs)]
+    y = fn(*xs)
+    (y * dev(gout, device, y.dtype)).sum().backward()
+    return host(y), [host(x.grad) for x in xs]
+
+
+# ------------------------------------------------------------- conversions
+def test_conversions(gpu_device):
+    import lie_vae.lie_tools as lt
+    g = golden("conversions.npz")
+    d = gpu_device
+    for tag in ("", "_small", "_large"):
+        y, (gv,) = grad_run(lt.rodrigues, [g[f"exp_v{tag}"]], g[f"exp_gR{tag}"], d)
+        assert_normwise(y, g[f"exp_R{tag}"], what=f"rodrigues{tag}")
+        assert_normwise(gv, g[f"exp_gv{tag}"], 1e-4, what=f"rodrigues grad{tag}")
+    assert np.isnan(host(lt.rodrigues(torch.zeros(1, 3, device=d)))).all()
+
+    q = host(lt.group_matrix_to_quaternions(dev(g["haar_R"], d)))
+    assert_normwise(q, g["haar_q"], what="mat->quat")
+    q = host(lt.group_matrix_to_quaternions(dev(g["gen_R"], d)))
+    assert_normwise(q, g["gen_q"], what="mat->quat generic")
+    y, (gr,) = grad_run(lt.group_matrix_to_eazyz, [g["haar_R"]], g["haar_gang"], d)
+    assert_normwise(y, g["haar_ang"], what="mat->eazyz")
+    assert_normwise(gr, g["haar_gR"], 1e-4, what="mat->eazyz grad")
+    _, (gr,) = grad_run(lt.group_matrix_to_quaternions, [g["gen_R"]], g["haar_gq"], d)
+    assert_normwise(gr, g["gen_gR"], 1e-4, what="mat->quat grad")
+    y, (gq,) = grad_run(lt.quaternions_to_eazyz, [g["q_unit"]], g["haar_gang"], d)
+    assert_normwise(y, g["q_eazyz"], what="quat->eazyz")
+    assert_normwise(gq, g["q_geazyz"], 1e-4, what="quat->eazyz grad")
+    y, (gq,) = grad_run(lt.quaternions_to_group_matrix, [g["q_in"]], g["q_gmat"], d)
+    assert_normwise(y, g["q_mat"], what="quat->mat")
+    assert_normwise(gq, g["q_gq"], 1e-4, what="quat->mat grad")
+    y, (ga, gc) = grad_run(lt.s2s1rodrigues, [g["s2s1_axis"], g["s2s1_cs"]], g["s2s1_gR"], d)
+    assert_normwise(y, g["s2s1_R"], what="s2s1")
+    assert_normwise(ga, g["s2s1_gaxis"], 1e-4, what="s2s1 grad axis")
+    assert_normwise(gc, g["s2s1_gcs"], 1e-4, what="s2s1 grad cs")
+    y, (g1, g2) = grad_run(lt.s2s2_gram_schmidt, [g["s2s2_v1"], g["s2s2_v2"]], g["s2s2_gR"], d)
+    assert_normwise(y, g["s2s2_R"], 1e-12, what="s2s2 fp64")
+    assert_normwise(g1, g["s2s2_gv1"], 1e-10, what="s2s2 grad v1")
+    assert_normwise(g2, g["s2s2_gv2"], 1e-10, what="s2s2 grad v2")
+    # edge rotations (identity, gimbal z-rotations, pi rotations): exact case choice
+    q = host(lt.group_matrix_to_quaternions(dev(g["edge_R"], d)))
+    np.testing.assert_allclose(q, g["edge_q"], rtol=1e-6, atol=1e-6)
+    ang = host(lt.group_matrix_to_eazyz(dev(g["edge_R"], d)))
+    np.testing.assert_allclose(ang, g["edge_ang"], rtol=1e-5, atol=1e-5)
+
+
+def test_empty_batches(gpu_device):
+    import lie_vae.lie_tools as lt
+    assert lt.rodrigues(torch.zeros(0, 3, device=gpu_device)).shape == (0, 3, 3)
+    out = lt.block_wigner_matrix_multiply(torch.zeros(0, 3, device=gpu_device),
+                                          torch.zeros(16, 4, device=gpu_device).expand(0, -1, -1), 3)
+    assert out.shape == (0, 16, 4)
+
+
+def test_bad_sizes_raise(gpu_device):
+    import lie_vae.lie_tools as lt
+    from lie_vae._lib import LieVaeHipError
+    a = torch.zeros(4, 3, device=gpu_device)
+    with pytest.raises(LieVaeHipError, match="l_max"):
+        lt.block_wigner_matrix_multiply(a, torch.zeros(4, 22 * 22, 2, device=gpu_device), 21)
+    with pytest.raises(LieVaeHipError, match="C must be"):
+        lt.block_wigner_matrix_multiply(a, torch.zeros(4, 16, 65, device=gpu_device), 3)
+
+
+# ------------------------------------------------------------------ Wigner-D
+def test_wigner_blocks_vs_golden(gpu_device):
+    import lie_vae.lie_tools as lt
+    g = golden("wigner.npz")
+    for l in range(11):
+        D = host(lt.wigner_d_matrix(dev(g["ang"], gpu_device), l))
+        assert_normwise(D, g[f"D{l}"], what=f"D{l}")
+    D = host(lt.wigner_d_matrix(dev(g["ang20"], gpu_device), 20))
+    assert_normwise(D, g["D20"], what="D20")
+
+
+@pytest.mark.parametrize("l", [0, 1, 2, 5, 10, 20])
+def test_wigner_properties(gpu_device, l):
+    """Reference property tests (lie_tools.py:337-357) on the HIP output."""
+    import lie_vae.lie_tools as lt
+    torch.manual_seed(l)
+    ra = lt.random_group_matrices(2000, device=gpu_device)
+    rb = lt.random_group_matrices(2000, device=gpu_device)
+    wa = lt.wigner_d_matrix(lt.group_matrix_to_eazyz(ra), l)
+    wb = lt.wigner_d_matrix(lt.group_matrix_to_eazyz(rb), l)
+    wc = lt.wigner_d_matrix(lt.group_matrix_to_eazyz(ra.bmm(rb)), l)
+    eye = torch.eye(2 * l + 1, device=gpu_device).expand_as(wa)
+    torch.testing.assert_close(wa @ wa.transpose(-2, -1), eye, rtol=1e-4, atol=1e-5)
+    winv = lt.wigner_d_matrix(lt.group_matrix_to_eazyz(ra.transpose(1, 2).contiguous()), l)
+    torch.testing.assert_close(wa @ winv, eye, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(wb.bmm(wa), wc, rtol=1e-3, atol=1e-3)
+
+
+# ----------------------------------------------------------------- the action
+ACTION_FILES = sorted(glob.glob(os.path.join(GOLDEN, "action_*.npz")))
+
+
+def parse_case(name):
+    return [int(x[1:]) for x in name[:-4].split("_")[1:]]
+
+
+@pytest.mark.parametrize("path", ACTION_FILES, ids=[os.path.basename(p) for p in ACTION_FILES])
+def test_action_vs_golden(gpu_device, path):
+    import lie_vae.lie_tools as lt
+    name = os.path.basename(path)
+    L, C, t, p = parse_case(name)
+    g = golden(name)
+    n = g["ang"].shape[0]
+
+    def f(a, s):
+        sx = s if p else s.expand(n, -1, -1)
+        return lt.block_wigner_matrix_multiply(a, sx, L, transpose=bool(t))
+
+    y, (ga, gs) = grad_run(f, [g["ang"], g["spec"]], g["gout"], gpu_device)
+    assert_normwise(y, g["out"], what=f"{name} out")
+    if "out64" in g:
+        e_hip = normwise(y, g["out64"])
+        e_ref = normwise(g["out"], g["out64"])
+        assert e_hip.max() <= 2 * max(e_ref.max(), 1e-7), (e_hip.max(), e_ref.max())
+    assert_normwise(ga, g["gang"], 1e-4, what=f"{name} dangles")
+    if p:
+        assert_normwise(gs, g["gspec"], 1e-4, what=f"{name} dspectrum")
+    else:
+        assert_normwise(gs[None], g["gspec"][None], 1e-5, what=f"{name} dspectrum")
+
+
+@pytest.mark.parametrize("L,C,n,transpose", [(10, 10, 4096, False), (3, 10, 256, False),
+                                             (10, 10, 1000, True), (20, 10, 512, False),
+                                             (7, 64, 300, False), (5, 1, 777, False),
+                                             (15, 13, 257, True)])
+def test_action_vs_oracle(gpu_device, L, C, n, transpose):
+    """Seeded Haar angles at BASELINE size (config 2: B=4096, l=10, C=10) and ragged
+    sizes, against the CPU oracle on the same fp32 inputs."""
+    import lie_vae.lie_tools as lt
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(1234 + L + n)
+    q = torch.randn(n, 4, generator=gen)
+    ang = lie_ref.mat_to_eazyz(lie_ref.quat_to_mat(q))
+    spec = torch.randn((L + 1) ** 2, C, generator=gen)
+    ref = lie_ref.block_wigner_apply(ang, spec.expand(n, -1, -1), L, transpose)
+    out = lt.block_wigner_matrix_multiply(ang.to(gpu_device), spec.to(gpu_device).expand(n, -1, -1),
+                                          L, transpose)
+    assert_normwise(host(out), ref.numpy(), what=f"L{L} C{C} n{n}")
+
+
+def test_action_linearity_and_transpose(gpu_device):
+    """Size-independent properties at 65536 samples: linear in F; D^T D F = F."""
+    import lie_vae.lie_tools as lt
+    torch.manual_seed(5)
+    n, L, C = 65536, 10, 10
+    ang = lt.group_matrix_to_eazyz(lt.random_group_matrices(n, device=gpu_device))
+    f1 = torch.randn((L + 1) ** 2, C, device=gpu_device)
+    f2 = torch.randn((L + 1) ** 2, C, device=gpu_device)
+    o1 = lt.block_wigner_matrix_multiply(ang, f1.expand(n, -1, -1), L)
+    o2 = lt.block_wigner_matrix_multiply(ang, f2.expand(n, -1, -1), L)
+    o12 = lt.block_wigner_matrix_multiply(ang, (2 * f1 - f2).expand(n, -1, -1), L)
+    assert_normwise(host(o12), host(2 * o1 - o2), 1e-5, what="linearity")
+    back = lt.block_wigner_matrix_multiply(ang, o1, L, transpose=True)
+    assert_normwise(host(back), host(f1.expand(n, -1, -1)), 2e-5, what="D^T D F = F")
+    # norm preservation per degree block (D orthogonal)
+    torch.testing.assert_close(o1.norm(dim=(1, 2)), f1.norm().expand(n), rtol=1e-5, atol=0)
+
+
+def test_action_bf16_output(gpu_device):
+    import lie_vae._ops as ops
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(99)
+    n, L, C = 2048, 20, 10
+    ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n))
+    spec = torch.randn((L + 1) ** 2, C, generator=gen)
+    out = ops.group_action(ang.to(gpu_device), spec.to(gpu_device), L, out_dtype=torch.bfloat16)
+    ref = lie_ref.block_wigner_apply(ang[:256], spec.expand(256, -1, -1), L)
+    assert out.dtype == torch.bfloat16
+    assert_normwise(host(out[:256].float()), ref.numpy(), 4e-3, what="bf16 out")
+
+
+# --------------------------------------------------------------- fused path
+def test_fused_vs_golden(gpu_device):
+    import lie_vae._ops as ops
+    g = golden("fused_exp_action.npz")
+    d = gpu_device
+    out = ops.fused_exp_action(dev(g["mu"], d), dev(g["v"], d), dev(g["item_rep"], d), 10)
+    assert_normwise(host(out).reshape(len(g["out"]), -1), g["out"], what="fused")
+
+
+def test_fused_matches_modular_and_grads(gpu_device):
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    torch.manual_seed(3)
+    n, L, C = 4096, 10, 10
+    mu = lt.random_group_matrices(n, device=gpu_device)
+    v = torch.randn(n, 3, device=gpu_device) * 0.5
+    F = torch.randn((L + 1) ** 2, C, device=gpu_device)
+    gout = torch.randn(n, (L + 1) ** 2, C, device=gpu_device)
+    xs = [t.clone().requires_grad_(True) for t in (mu, v, F)]
+    y1 = ops.fused_exp_action(*xs, L)
+    (y1 * gout).sum().backward()
+    ys = [t.clone().requires_grad_(True) for t in (mu, v, F)]
+    z = ops.so3_sample(ys[0], ys[1][None])[0]
+    y2 = lt.block_wigner_matrix_multiply(lt.group_matrix_to_eazyz(z), ys[2].expand(n, -1, -1), L)
+    (y2 * gout).sum().backward()
+    assert_normwise(host(y1), host(y2), 2e-6, what="fused vs modular")
+    for a, b, w in zip(xs, ys, ("mu", "v", "F")):
+        assert_normwise(host(a.grad)[None], host(b.grad)[None], 1e-4, what=f"grad {w}")
+
+
+def test_fused_vs_oracle_config2(gpu_device):
+    """Config 2 exactly: B=4096, l=10, C=10, v ~ N(0,1), shared F (no mu)."""
+    import lie_vae._ops as ops
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(0)
+    n, L, C = 4096, 10, 10
+    v = torch.randn(n, 3, generator=gen)
+    F = torch.randn((L + 1) ** 2, C, generator=gen)
+    ref = lie_ref.block_wigner_apply(lie_ref.mat_to_eazyz(lie_ref.so3_exp(v)),
+                                     F.expand(n, -1, -1), L)
+    out = ops.fused_exp_action(None, v.to(gpu_device), F.to(gpu_device), L)
+    assert_normwise(host(out), ref.numpy(), what="config2 fused")
+
+
+# ---------------------------------------------------------------- reparam
+@pytest.mark.parametrize("mode", ["alg", "s2s2", "q", "s2s1"])
+def test_so3_reparam_vs_golden(gpu_device, mode):
+    import lie_vae.reparameterize as rp
+    g = golden("reparam.npz")
+    mean_cls = {"alg": rp.AlgebraMean, "s2s2": rp.S2S2Mean, "q": rp.QuaternionMean,
+                "s2s1": rp.S2S1Mean}[mode]
+    rep = rp.SO3reparameterize(rp.N0reparameterize(10, z_dim=3), mean_cls(10), k=10)
+    with torch.no_grad():
+        for name, p in rep.named_parameters():
+            p.copy_(torch.from_numpy(g[f"{mode}_p_{name}"]))
+    rep = rep.to(gpu_device)
+    h = dev(g[f"{mode}_h"], gpu_device).requires_grad_(True)
+    eps = dev(g[f"{mode}_eps"], gpu_device)
+    z = rep(h, 2, eps=eps)
+    assert_normwise(host(rep.mu_lie), g[f"{mode}_mu"], what="mu")
+    assert_normwise(host(rep.v).reshape(-1, 3), g[f"{mode}_v"].reshape(-1, 3), what="v")
+    assert_normwise(host(z).reshape(-1, 9), g[f"{mode}_z"].reshape(-1, 9), what="z")
+    lp = host(rep.log_posterior())
+    np.testing.assert_allclose(lp, g[f"{mode}_logpost"], rtol=1e-5, atol=1e-4)
+    kl = rep.kl()
+    np.testing.assert_allclose(host(kl), g[f"{mode}_kl"], rtol=1e-5, atol=1e-4)
+    ((z * dev(g[f"{mode}_gz"], gpu_device)).sum() +
+     (kl * dev(g[f"{mode}_gk"], gpu_device)).sum()).backward()
+    assert_normwise(host(h.grad)[None], g[f"{mode}_gh"][None], 1e-4, what="dh")
+    for name, p in rep.named_parameters():
+        assert_normwise(host(p.grad)[None], g[f"{mode}_g_{name}"][None], 1e-4, what=f"d{name}")
+
+
+def test_log_posterior_wide_range(gpu_device):
+    import lie_vae._ops as ops
+    g = golden("reparam.npz")
+    v = dev(g["lp_v"], gpu_device).requires_grad_(True)
+    s = dev(g["lp_sigma"], gpu_device).requires_grad_(True)
+    lp = ops.so3_log_posterior(v, s, 10)
+    np.testing.assert_allclose(host(lp), g["lp_out"], rtol=1e-5, atol=1e-4)
+    (lp * dev(g["lp_g"], gpu_device)).sum().backward()
+    assert_normwise(host(v.grad).reshape(-1, 3), g["lp_gv"].reshape(-1, 3), 1e-4, what="gv")
+    assert_normwise(host(s.grad)[None], g["lp_gsigma"][None], 1e-4, what="gsigma")
