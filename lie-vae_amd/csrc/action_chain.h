@@ -132,12 +132,12 @@ constexpr int j_nnz() {
   return c;
 }
 
-// Make this wave's LDS writes visible to its own later reads (and keep the compiler
-// from moving LDS traffic across the point).
+// Make this wave's LDS writes visible to its own later reads (cross-lane, same wave).
+// Only LDS is waited for: a workgroup-scope release fence would also emit
+// s_waitcnt vmcnt(0) and stall on every global store still in flight.  The "memory"
+// clobber keeps the compiler from moving LDS or global accesses across this point.
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 }  // namespace lv

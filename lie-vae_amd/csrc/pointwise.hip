@@ -377,7 +377,7 @@ int lv_so3_sample_bwd(const float* mu, const float* v, const float* gz, float* g
   LV_CHECK_ARG(ns >= 0 && B >= 0, "bad sizes");
   LV_PTRS(mu && v && gz && gmu && gv);
   if (ns == 0) {
-    hipMemsetAsync(gmu, 0, sizeof(float) * 9 * B, (hipStream_t)stream);
+    (void)hipMemsetAsync(gmu, 0, sizeof(float) * 9 * B, (hipStream_t)stream);
     return LV_OK;
   }
   LV_LAUNCH1(so3_sample_bwd_k, n, mu, v, gz, gmu, gv, ns, B);
@@ -469,7 +469,7 @@ int lv_so3_log_posterior_bwd(const float* v, const float* sigma, const float* go
   LV_CHECK_ARG(k >= 0 && k <= kMaxWrap, "k must be in [0, %d]", kMaxWrap);
   LV_PTRS(v && sigma && gout && gv && gsigma);
   if (ns == 0) {
-    hipMemsetAsync(gsigma, 0, sizeof(float) * 3 * B, (hipStream_t)stream);
+    (void)hipMemsetAsync(gsigma, 0, sizeof(float) * 3 * B, (hipStream_t)stream);
     return LV_OK;
   }
   LV_LAUNCH1(so3_logpost_bwd_k, n, v, sigma, gout, gv, gsigma, ns, B, k);

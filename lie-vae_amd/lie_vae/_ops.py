@@ -216,8 +216,8 @@ def group_action(angles, spectrum, L, transpose=False, out_dtype=F32):
     C = spectrum.shape[-1]
     assert spectrum.shape[-2] == M, f"spectrum rows {spectrum.shape[-2]} != (L+1)^2 = {M}"
     if spectrum.dim() == 3 and spectrum.stride(0) == 0:
-        # (M,C) passed once; autograd routes dF through select+expand back to item_rep
-        spectrum = spectrum[0]
+        # (M,C) passed once; autograd routes dF through expand back to item_rep
+        spectrum = spectrum.as_strided(spectrum.shape[1:], spectrum.stride()[1:])
     return _GroupAction.apply(angles, _contig(spectrum), L, transpose, out_dtype)
 
 
