@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
                     help="graph: steps captured in a hipGraph and replayed; eager: C launch loop")
     ap.add_argument("--graph-chunk", type=int, default=100)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="independent batches in flight on this many HIP streams (graph mode)")
+    ap.add_argument("--multistream", type=int, default=4,
+                    help="also time this many independent batches in flight (extra field)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="also print a batch sweep (stderr)")
@@ -100,13 +104,16 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     v = torch.randn(B, 3, generator=g).to(dev)
     F = torch.randn(M, C, generator=g).to(dev)
-    out = torch.empty(B, M, C, device=dev, dtype=out_dtype)
+    nstreams = max(1, args.streams if args.launch == "graph" else 1)
+    outs = [torch.empty(B, M, C, device=dev, dtype=out_dtype) for _ in range(nstreams)]
+    out = outs[0]
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
-    def launch(k, s=sp):
-        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(v), P(F), 0, P(out), dt, None, B, L, C, 0,
+    def launch(k, s=sp, o=None):
+        o = out if o is None else o
+        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(v), P(F), 0, P(o), dt, None, B, L, C, 0,
                                                 k, s)
         if rc:
             raise RuntimeError(_lib.last_error())
@@ -119,8 +126,19 @@ def main():
         s = torch.cuda.Stream(dev)
         s.wait_stream(stream)
         graph = torch.cuda.CUDAGraph()
+        if nstreams > 1:
+            chunk = max(nstreams, chunk - chunk % nstreams)
+            side = [torch.cuda.Stream(dev) for _ in range(nstreams)]
         with torch.cuda.graph(graph, stream=s):
-            launch(chunk, ctypes.c_void_p(s.cuda_stream))
+            if nstreams == 1:
+                launch(chunk, ctypes.c_void_p(s.cuda_stream))
+            else:  # fork: independent batches on parallel graph branches, then join
+                for t in side:
+                    t.wait_stream(s)
+                for t, o in zip(side, outs):
+                    launch(chunk // nstreams, ctypes.c_void_p(t.cuda_stream), o)
+                for t in side:
+                    s.wait_stream(t)
         torch.cuda.synchronize(dev)
 
     def run_steps(k):
@@ -180,6 +198,42 @@ def main():
             del vv, oo
         print(json.dumps({"sweep": sweep}), file=sys.stderr)
 
+    # independent batches on parallel streams (same kernel): aggregate throughput
+    multi = None
+    if args.launch == "graph" and nstreams == 1 and args.multistream > 1:
+        ms = args.multistream
+        mouts = [torch.empty(B, M, C, device=dev, dtype=out_dtype) for _ in range(ms)]
+        side = [torch.cuda.Stream(dev) for _ in range(ms)]
+        mchunk = max(ms, chunk - chunk % ms)
+        g2 = torch.cuda.CUDAGraph()
+        s2 = torch.cuda.Stream(dev)
+        s2.wait_stream(stream)
+        with torch.cuda.graph(g2, stream=s2):
+            for t in side:
+                t.wait_stream(s2)
+            for t, o in zip(side, mouts):
+                launch(mchunk // ms, ctypes.c_void_p(t.cuda_stream), o)
+            for t in side:
+                s2.wait_stream(t)
+        reps = max(1, args.steps // mchunk)
+        for _ in range(2):
+            g2.replay()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            g2.replay()
+        torch.cuda.synchronize(dev)
+        el2 = time.perf_counter() - t1
+        multi = {"streams": ms, "steps": reps * mchunk, "value": reps * mchunk * B * world / el2,
+                 "unit": "samples/s", "us_per_step": el2 / (reps * mchunk) * 1e6,
+                 "aggregate_GBs": abytes * reps * mchunk / el2 / 1e9}
+        del mouts
+
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", f"traffic_B{B}_L{L}_C{C}_{args.dtype}.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(L, C, B, args.cpu_seconds)
@@ -202,12 +256,13 @@ def main():
                                    "(lv_fused_exp_action_fwd)",
                        "batch_per_gpu": B, "global_batch": B * world, "l_max": L,
                        "channels": C, "parallelism": f"sample-sharded x{world}, no collective",
-                       "launch": args.launch},
+                       "launch": args.launch, "streams": nstreams},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": abytes,
                          "us_per_launch_events": per_launch_s * 1e6},
             "cpu_baseline": cpu,
+            "multistream": multi,
         }
         print(json.dumps(rec), flush=True)
     if dist:

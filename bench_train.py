@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Training-step benchmark for BASELINE configs 3 and 4 (not the driver's bench.py).
+
+Config 3: the full sphere-cube VAE (ConvNetBN encoder -> SO(3) reparam with S2S2 mean
+-> action decoder l=10, C=10 -> DeconvNet(hidden 200), RGB 64x64), batch 512, one GPU.
+Config 4: the same model, global batch 4096 data-parallel over N GPUs (512 per rank),
+RCCL all-reduce of the gradients (lie_vae.experiments.train_dp).
+
+One step = elbo forward (n=1) + backward + global-norm clip (1e-5) + Adam (lr 1e-3) —
+the reference step of unsupervised.py:69-117 without its per-step host syncs.  Inputs:
+synthetic x ~ U[0,1)^(B x 3 x 64 x 64) resident in HBM (the sphere-cube renders are not
+available offline), seeded per rank.
+
+  python bench_train.py                      # config 3
+  torchrun --nproc-per-node 8 bench_train.py --global-batch 4096    # config 4
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "lie-vae_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--global-batch", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--lmax", type=int, default=10)
+    ap.add_argument("--deconv-hidden", type=int, default=200)
+    ap.add_argument("--mean-mode", default="s2s2")
+    ap.add_argument("--channels-last", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from lie_vae.experiments.train_dp import DPTrainer, param_count
+    from lie_vae.experiments.vae import VAE
+
+    torch.manual_seed(0)
+    model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,
+                rgb=True, batch_norm=True, deconv_hidden=args.deconv_hidden,
+                mean_mode=args.mean_mode).to(dev)
+    if args.channels_last:
+        model = model.to(memory_format=torch.channels_last)
+    trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5)
+    B = args.global_batch // world
+    g = torch.Generator(device="cpu").manual_seed(100 + rank)
+    x = torch.rand(B, 3, 64, 64, generator=g).to(dev)
+
+    for _ in range(args.warmup):
+        trainer.step(x)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, recon, kl = trainer.step(x)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "VAE train samples/s (conv enc + SO(3) reparam + action dec, l=10)",
+            "value": args.global_batch * args.steps / el, "unit": "samples/s", "n_gpus": world,
+            "steps": args.steps, "ms_per_step": el * 1e3 / args.steps,
+            "config": {"global_batch": args.global_batch, "per_gpu": B, "l_max": args.lmax,
+                       "deconv_hidden": args.deconv_hidden, "mean_mode": args.mean_mode,
+                       "params": param_count(model), "dtype": "f32"},
+            "loss": float(loss.item()), "recon": float(recon.mean().item()),
+            "kl": float(kl.mean().item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

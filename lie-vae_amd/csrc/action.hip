@@ -73,11 +73,12 @@ inline int plan_segments(int L, int nseg, double P, bool bwd, int* seg_lo) {
   return nseg;
 }
 
-// Segments so that the grid has ~2 waves per SIMD (1024 SIMDs on MI355X), but never
-// more ranges than pay for their duplicated prologue.
+// Segments so that the grid has ~2.7 waves per SIMD (1024 SIMDs on MI355X; measured
+// best at batch 4096, l = 10: 4 segments), but never more ranges than pay for their
+// duplicated prologue.
 inline int choose_nseg(int64_t n, int Sw, int L, double P, bool bwd) {
   const int64_t waves = (n + Sw - 1) / Sw;
-  const int64_t target = 2048;
+  const int64_t target = 2732;
   int nseg = (int)std::min<int64_t>(kMaxSeg, std::max<int64_t>(1, (target + waves - 1) / waves));
   // cap: a range should carry at least ~2x its prologue
   double total = 0.0;
@@ -86,8 +87,8 @@ inline int choose_nseg(int64_t n, int Sw, int L, double P, bool bwd) {
   return std::min(nseg, std::min(cap, L + 1));
 }
 
-constexpr double kPrologueFwd = 220.0;
-constexpr double kPrologueFused = 420.0;
+constexpr double kPrologueFwd = 200.0;
+constexpr double kPrologueFused = 250.0;
 
 template <template <int> class Launcher, int LT = 0>
 int dispatch_L(int L, typename Launcher<0>::Args& args) {

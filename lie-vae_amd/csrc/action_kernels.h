@@ -20,6 +20,28 @@
 #include "action_chain.h"
 #include "so3_device.h"
 
+// Diagnostic timestamps (tools/kbench.hip builds with -DLV_STAMPS; never in the library).
+#ifndef LV_STORE_MODE
+#define LV_STORE_MODE 0
+#endif
+#ifndef LV_PROLOGUE_MODE
+#define LV_PROLOGUE_MODE 0
+#endif
+#ifdef LV_STAMPS
+__device__ unsigned long long* lv_stamp_buf;
+#define LV_STAMP(slot)                                                                  \
+  do {                                                                                  \
+    if ((threadIdx.x & 63) == 0) {                                                      \
+      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                   \
+      const unsigned long long w_ = ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * \
+                                    (blockDim.x >> 6) + (threadIdx.x >> 6);             \
+      lv_stamp_buf[w_ * 8 + (slot)] = t_;                                               \
+    }                                                                                   \
+  } while (0)
+#else
+#define LV_STAMP(slot) do {} while (0)
+#endif
+
 namespace lv {
 
 constexpr int kWavesPerBlock = 4;
@@ -40,9 +62,11 @@ struct ActionArgs {
   int seg_lo[kMaxSeg + 1];
 };
 
-// ZYZ (cos, sin) straight from the quaternion, same function as
-// quaternions_to_eazyz (lie_tools.py:160-175) followed by cos/sin: atan2(y, x) ->
-// (x, y)/hypot, acos(clamp(w)) -> (w, sqrt((1-w)(1+w))).  atan2(0, 0) edge mirrored.
+// ---- fused-prologue maths (per lane, registers).
+
+// ZYZ (cos, sin) straight from the quaternion: the function quaternions_to_eazyz
+// (lie_tools.py:160-175) followed by cos/sin.  atan2(y, x) -> (x, y)/|(x, y)| with the
+// atan2(+-0, +-0) edge mirrored; acos(clamp(w)) -> (w, sqrt((1-w)(1+w))).
 __device__ __forceinline__ void quat_to_zyz_trig(const float q[4], float c1[3], float s1[3]) {
   const float a1 = q[1] * q[2] - q[0] * q[3];
   const float b1 = q[0] * q[2] + q[1] * q[3];
@@ -50,11 +74,12 @@ __device__ __forceinline__ void quat_to_zyz_trig(const float q[4], float c1[3], 
   const float a3 = q[0] * q[3] + q[1] * q[2];
   const float b3 = q[1] * q[3] - q[0] * q[2];
   auto dir = [](float y, float x, float& c, float& s) {
-    if (x == 0.f && y == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
+    const float r2 = x * x + y * y;
+    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
       c = signbit(x) ? -1.f : 1.f;
       s = 0.f;
     } else {
-      const float r = rhypotf(x, y);
+      const float r = rsqrtf(r2);
       c = x * r;
       s = y * r;
     }
@@ -66,40 +91,116 @@ __device__ __forceinline__ void quat_to_zyz_trig(const float q[4], float c1[3], 
   dir(a3, b3, c1[2], s1[2]);
 }
 
-// Per-lane angle setup; returns (cos, sin) of the three chain angles.  For transpose
-// (D^T = X(-c) J X(-b) J X(-a)) the slots are swapped and the sines negated.
+// The same (cos, sin) for z = exp(v) straight from the axis-angle form, at better than
+// fp32-reference accuracy.  The reference's q = group_matrix_to_quaternions(rodrigues(v))
+// is, in exact arithmetic, the unit quaternion q* = (-u sin(t/2), cos(t/2)) of R(v) (its
+// matrix is the transpose of the active one) with the trace method's epsilon applied to
+// the largest component k: q_k -> d = sqrt(q_k^2 + 2.5e-7), q_j -> sign(q_k) q_j |q_k| / d
+// (lie_tools.py:126-156).  cos(beta) = 1 - (1 - cb) is formed in "one-minus" form so that
+// sin(beta) = sqrt((1-cb)(1+cb)) keeps full relative accuracy near beta = 0 / pi, where the
+// reference's fp32 acos(cb) loses it (the clamp to +-(1 - 1e-6) is mirrored exactly).
+__device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], float s1[3],
+                                                float qr[4]) {
+  const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const float inv = rsqrtf(vv);  // NaN downstream at v = 0, as the reference
+  const float th = vv * inv;
+  float sh, ch;
+  sincosf(0.5f * th, &sh, &ch);
+  const float m = -sh * inv;
+  const float qt[4] = {v[0] * m, v[1] * m, v[2] * m, ch};
+  int k = 0;
+  float best = fabsf(qt[0]);
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (fabsf(qt[i]) > best) { best = fabsf(qt[i]); k = i; }
+  const float qk = k == 0 ? qt[0] : (k == 1 ? qt[1] : (k == 2 ? qt[2] : qt[3]));
+  constexpr float eps = 2.5e-7f;
+  const float qk2 = qk * qk;
+  const float d = sqrtf(qk2 + eps);
+  const float sc = copysignf(best / d, qk);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
+  const float oms = eps * (1.f - 2.f * qk2 - eps) / (qk2 + eps);  // 1 - |q_ref|^2
+  float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
+  float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
+  constexpr float kDelta = 1.f - kEazyzHi;                          // exact in fp32
+  if (omc < kDelta) { omc = kDelta; opc = 2.f - kDelta; }
+  else if (opc < kDelta) { opc = kDelta; omc = 2.f - kDelta; }
+  c1[1] = omc <= opc ? 1.f - omc : opc - 1.f;
+  s1[1] = sqrtf(omc * opc);
+  auto dir = [](float y, float x, float& c, float& s) {
+    const float r2 = x * x + y * y;
+    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
+      c = signbit(x) ? -1.f : 1.f;
+      s = 0.f;
+    } else {
+      const float r = rsqrtf(r2);
+      c = x * r;
+      s = y * r;
+    }
+  };
+  dir(qr[1] * qr[2] - qr[0] * qr[3], qr[0] * qr[2] + qr[1] * qr[3], c1[0], s1[0]);
+  dir(qr[0] * qr[3] + qr[1] * qr[2], qr[1] * qr[3] - qr[0] * qr[2], c1[2], s1[2]);
+}
+
+// Per-lane inputs, loaded before the block barrier so that their latency overlaps the
+// spectrum staging.
+struct LaneIn {
+  float v[3];
+  float mu[9];
+};
+
 template <bool FUSED>
-__device__ __forceinline__ void lane_angles(const ActionArgs& a, int64_t s, bool active, int c,
-                                            bool write_ang, float c1[3], float s1[3]) {
-  float cc[3] = {1.f, 1.f, 1.f}, ss[3] = {0.f, 0.f, 0.f};
-  if (active) {
-    if constexpr (FUSED) {
-      float v[3] = {a.v[s * 3 + 0], a.v[s * 3 + 1], a.v[s * 3 + 2]};
+__device__ __forceinline__ void lane_load(const ActionArgs& a, int64_t s, LaneIn& in) {
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in.v[i] = a.v[s * 3 + i];
+    if (a.mu) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) in.mu[i] = a.mu[s * 9 + i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in.v[i] = a.ang[s * 3 + i];
+  }
+}
+
+// (cos, sin) of the three chain angles.  For transpose (D^T = X(-c) J X(-b) J X(-a)) the
+// slots are swapped and the sines negated.
+template <bool FUSED>
+__device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& in, int64_t s,
+                                            bool active, int c, bool write_ang, float c1[3],
+                                            float s1[3]) {
+  float cc[3], ss[3];
+#if LV_PROLOGUE_MODE == 1  // diagnostic: trivial angles (loads kept)
+  if (true) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { cc[i] = in.v[i]; ss[i] = in.v[(i + 1) % 3]; }
+  } else
+#endif
+  if constexpr (FUSED) {
+    float q[4];
+    if (a.mu) {
+      // general mean: the reference's own fp32 sequence (exact division / sqrt, as the
+      // stand-alone conversion kernels), so the result tracks its rounding closely
       float R[9], z[9];
-      rodrigues_fwd(v, R);
-      if (a.mu) {
-        float mu[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) mu[i] = a.mu[s * 9 + i];
-        matmul3(mu, R, z);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) z[i] = R[i];
-      }
-      float q[4];
+      rodrigues_fwd(in.v, R);
+      matmul3(in.mu, R, z);
       mat_to_quat_fwd(z, q, nullptr);
       quat_to_zyz_trig(q, cc, ss);
-      if (write_ang && c == 0) {
-        float ang[3];
-        quat_to_eazyz_fwd(q, ang);
-        a.ang_out[s * 3 + 0] = ang[0];
-        a.ang_out[s * 3 + 1] = ang[1];
-        a.ang_out[s * 3 + 2] = ang[2];
-      }
     } else {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) sincosf(a.ang[s * 3 + i], &ss[i], &cc[i]);
+      exp_to_zyz_trig(in.v, cc, ss, q);
     }
+    if (write_ang && active && c == 0) {
+      float ang[3];
+      quat_to_eazyz_fwd(q, ang);
+      a.ang_out[s * 3 + 0] = ang[0];
+      a.ang_out[s * 3 + 1] = ang[1];
+      a.ang_out[s * 3 + 2] = ang[2];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sincosf(in.v[i], &ss[i], &cc[i]);
   }
   if (a.transpose) {
     c1[0] = cc[2]; s1[0] = -ss[2];
@@ -116,16 +217,80 @@ __device__ __forceinline__ void lane_angles(const ActionArgs& a, int64_t s, bool
 // to an odd count so that the C columns fall in different banks.
 __host__ __device__ inline int fseg_rows(int lo, int hi) { return (hi * hi - lo * lo) | 1; }
 
-// Forward.  Per degree each lane runs the factored chain on its column and stores its
-// (2l+1) outputs straight from registers: one store instruction per output row puts
-// Sw contiguous C-float pieces (one per sample) in flight; consecutive rows of a sample
-// are adjacent, so L2 merges them into whole lines before they reach HBM.  There is no
-// load after the first store (vmcnt retires in order, so a later load would wait for
-// every older store): a shared spectrum is staged into LDS up front and a per-sample
-// spectrum is prefetched one degree ahead.
-template <int LT, bool FUSED, bool SHARED, typename OutT>
+// Output staging.  Degrees are written back in chunks: {0..3} (16 rows), {4, 5} (20 rows),
+// then one degree per chunk.  A chunk of a wave's Sw samples sits in LDS as [j][row][c]
+// with a per-sample stride SP = C (mod 32) -- lanes (j, c) then hit 64 distinct banks --
+// and is written back as Sw contiguous runs of rows*C values with 8-byte stores.
+__host__ __device__ constexpr int chunk_first(int l) { return l <= 3 ? 0 : (l <= 5 ? 4 : l); }
+__host__ __device__ constexpr int chunk_rows_max(int L) {
+  return (L >= 6 ? 2 * L + 1 : 0) > 20 ? 2 * L + 1 : 20;
+}
+__host__ __device__ inline int stage_stride(int L, int C) {
+  return ((chunk_rows_max(L) * C + 31) & ~31) + C;
+}
+__host__ __device__ inline int stage_floats(int L, int C) { return (64 / C) * stage_stride(L, C); }
+
+// Write a staged chunk back: Sv runs of rows*C values, run j from stage + j*SP to
+// out[(s0+j)*MC + row0*C ...].  Latency-tolerant form: every lane first issues all its
+// LDS reads (K = at most chunk_rows_max/2 float2 per lane, since Sw*C <= 64), waits
+// once, then issues its stores -- 512 contiguous bytes per wave instruction.
+template <int K, typename OutT>
+__device__ __forceinline__ void flush_chunk(const float* stage, int SP, OutT* out, int64_t s0,
+                                            int64_t MC, int row0, int rows, int C, int Sv,
+                                            int lane) {
+  const int plen = rows * C;
+  if ((C & 1) == 0) {
+    const int npair = plen >> 1;
+    const int total = Sv * npair;
+    // (j, w) of element e = lane + 64k, tracked incrementally
+    int j = 0, w = lane;
+    while (w >= npair) { w -= npair; ++j; }
+    float2 v[K];
+    int jj[K], ww[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      jj[k] = j;
+      ww[k] = w;
+      if (lane + 64 * k < total)
+        v[k] = *reinterpret_cast<const float2*>(stage + j * SP + 2 * w);
+      w += 64;
+      while (w >= npair) { w -= npair; ++j; }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (lane + 64 * k < total) {
+        OutT* dst = out + (s0 + jj[k]) * MC + (int64_t)row0 * C + 2 * ww[k];
+        if constexpr (sizeof(OutT) == 4) {
+          *reinterpret_cast<float2*>(dst) = v[k];
+        } else {
+          __hip_bfloat162 h;
+          h.x = __float2bfloat16(v[k].x);
+          h.y = __float2bfloat16(v[k].y);
+          *reinterpret_cast<__hip_bfloat162*>(dst) = h;
+        }
+      }
+    }
+  } else {
+    for (int j = 0; j < Sv; ++j) {
+      const float* src = stage + j * SP;
+      OutT* dst = out + (s0 + j) * MC + (int64_t)row0 * C;
+      for (int w = lane; w < plen; w += 64) store_out(dst + w, src[w]);
+    }
+  }
+}
+
+// Forward.  Per degree each lane runs the factored chain on its column and parks its
+// (2l+1) outputs in the wave's LDS stage; at the end of a chunk the stage is written back
+// as contiguous runs.  There is no global load after the first store (vmcnt retires in
+// order, so a later load would wait for every older store): a shared spectrum is staged
+// into LDS up front and a per-sample spectrum is prefetched one degree ahead.
+#ifndef LV_STAGED_DEFAULT
+#define LV_STAGED_DEFAULT false
+#endif
+template <int LT, bool FUSED, bool SHARED, typename OutT, bool STAGED = LV_STAGED_DEFAULT>
 __global__ __launch_bounds__(kThreads) void action_fwd_kernel(ActionArgs a) {
   extern __shared__ float lds[];
+  LV_STAMP(0);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int C = a.C, Sw = a.Sw;
@@ -133,31 +298,57 @@ __global__ __launch_bounds__(kThreads) void action_fwd_kernel(ActionArgs a) {
   const int c = lane - j * C;
   const int lo = a.seg_lo[blockIdx.y], hi = a.seg_lo[blockIdx.y + 1];
   const int rows_lo = lo * lo;
-  const int frows = fseg_rows(lo, hi);
+  const int frows = SHARED ? fseg_rows(lo, hi) : 0;
+  const int64_t s0 = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * Sw;
+  const int Sv = (int)max((int64_t)0, min((int64_t)Sw, a.n - s0));
+  const bool active = j < Sv;
+  const int64_t s = active ? s0 + j : (Sv > 0 ? s0 : 0);  // idle lanes mirror a valid sample
+  LaneIn in;
+  if (Sv > 0) lane_load<FUSED>(a, s, in);
+  // Shared spectrum slice: loads issued now, LDS writes and the barrier after the
+  // prologue maths so that both memory latencies overlap the per-lane arithmetic.
+  constexpr int kFPer = 8;  // staged values per thread (bounded; a loop covers larger slices)
+  float fv[kFPer];
+  const int fcnt = SHARED ? (hi * hi - rows_lo) * C : 0;
+  const float* fsrc = a.F + rows_lo * C;
   if constexpr (SHARED) {
-    const float* src = a.F + rows_lo * C;
-    const int cnt = (hi * hi - rows_lo) * C;
-    for (int e = threadIdx.x; e < cnt; e += kThreads) {
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      fv[k] = e < fcnt ? fsrc[e] : 0.f;
+    }
+  }
+  float c1[3], s1[3];
+  TrigTab<LT> t;
+  if (Sv > 0) {
+    lane_angles<FUSED>(a, in, s, active, c, FUSED && a.ang_out && blockIdx.y == 0, c1, s1);
+    trig_fill<LT>(t, c1, s1, hi - 1);
+  }
+  LV_STAMP(1);
+  if constexpr (SHARED) {
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      if (e < fcnt) {
+        const int r = e / C, cc = e - r * C;
+        lds[cc * frows + r] = fv[k];
+      }
+    }
+    for (int e = threadIdx.x + kFPer * kThreads; e < fcnt; e += kThreads) {
       const int r = e / C, cc = e - r * C;
-      lds[cc * frows + r] = src[e];
+      lds[cc * frows + r] = fsrc[e];
     }
     __syncthreads();
   }
-  const int64_t s0 = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * Sw;
-  if (s0 >= a.n) return;  // whole wave idle (no block barriers below)
-  const int Sv = (int)min((int64_t)Sw, a.n - s0);
-  const int64_t s = s0 + j;
-  const bool active = j < Sv;
+  LV_STAMP(2);
+  if (Sv == 0) return;  // whole wave idle (no block barriers below)
 
-  float c1[3], s1[3];
-  lane_angles<FUSED>(a, s, active, c, FUSED && a.ang_out && blockIdx.y == 0, c1, s1);
-  TrigTab<LT> t;
-  trig_fill<LT>(t, c1, s1, hi - 1);
-
-  OutT* dst = reinterpret_cast<OutT*>(a.out) + (active ? s * a.MC + c : 0);
+  const int SP = stage_stride(LT, C);
+  float* stage = lds + (SHARED ? ((frows * C + 3) & ~3) : 0) + (STAGED ? wave * stage_floats(LT, C) : 0);
+  float* stage_lane = stage + j * SP + c;
+  OutT* out = reinterpret_cast<OutT*>(a.out);
   const float* Fl = lds + c * frows - rows_lo;                  // shared: LDS column
-  // per-sample: global; idle lanes read sample s0's column (valid memory, result unused)
-  const float* Fs = a.F + (active ? s : s0) * a.Fstride + c;
+  const float* Fs = a.F + s * a.Fstride + c;                    // per-sample: global
   float fpre[SHARED ? 1 : 2 * LT + 1];
 
   sfor<LT + 1>([&](auto Lc) {
@@ -181,20 +372,69 @@ __global__ __launch_bounds__(kThreads) void action_fwd_kernel(ActionArgs a) {
           }
         }
       }
+#if LV_STORE_MODE == 3  // diagnostic: no chain, spectrum stored as is
+#pragma unroll
+      for (int i = 0; i < nn; ++i) y[i] = x[i] * c1[0];
+#else
       xrot<l, 2>(t, x, y);
       jmul<l>(y, x);
       xrot<l, 1>(t, x, y);
       jmul<l>(y, x);
       xrot<l, 0>(t, x, y);
-      if (active) {
-        OutT* d = dst + r0 * C;
+#endif
+#if LV_STORE_MODE == 1  // diagnostic: no stores, outputs kept live
+#pragma unroll
+      for (int i = 0; i < nn; ++i) asm volatile("" ::"v"(y[i]));
+#else
+      if constexpr (STAGED) {
+        // chunk this degree belongs to, clipped to the segment
+        constexpr int cf = chunk_first(l);
+        const int first = cf > lo ? cf : lo;
+        const int crow0 = first * first;
+        if (active) {
+          float* d = stage_lane + (r0 - crow0) * C;
+          sfor<nn>([&](auto I) {
+            d[0] = y[LV_CV(I)];
+            d += C;
+          });
+        }
+        constexpr bool chunk_end = (l == LT) || (chunk_first(l + 1) == l + 1);
+        if (chunk_end || l + 1 == hi) {
+          wave_lds_sync();
+          flush_chunk<(chunk_rows_max(LT) + 1) / 2, OutT>(stage, SP, out, s0, a.MC, crow0,
+                                                           r0 + nn - crow0, C, Sv, lane);
+          wave_lds_sync();
+        }
+      } else if ((C & 1) == 0) {
+        // Row pairs: adjacent lanes (c even, c+1) swap one value (DPP quad_perm, no LDS)
+        // so that even lanes store (row i, cols c..c+1) and odd lanes (row i+1, cols
+        // c-1..c): one 8-byte store per lane writes two whole rows of every sample
+        // (80-B runs at C = 10).  A pair never straddles samples since C is even.
+        const bool odd = (c & 1) != 0;
+        OutT* d = out + s * a.MC + r0 * C + (odd ? C + c - 1 : c);
+        sfor<nn / 2>([&](auto P) {
+          constexpr int i = 2 * LV_CV(P);
+          const float send = odd ? y[i] : y[i + 1];
+          const float recv = dpp_swap_adjacent(send);
+          const float v0 = odd ? recv : y[i];
+          const float v1 = odd ? y[i + 1] : recv;
+          if (active) store_out2(d, v0, v1);
+          d += 2 * C;
+        });
+        if (active) store_out(out + s * a.MC + (r0 + nn - 1) * C + c, y[nn - 1]);
+      } else if (active) {
+        // one store per output row: Sw contiguous C-value pieces per instruction; a
+        // sample's rows are adjacent, so L2 merges them into whole lines
+        OutT* d = out + s * a.MC + r0 * C + c;
         sfor<nn>([&](auto I) {
           store_out(d, y[LV_CV(I)]);
           d += C;
         });
       }
+#endif
     }
   });
+  LV_STAMP(3);
 }
 
 // ---------------------------------------------------------------- backward
@@ -420,8 +660,8 @@ struct FwdLauncher {
     const bool shared = p.a.Fstride == 0;
     if (shared)
       for (int k = 0; k < p.gy; ++k)
-        fmax = max(fmax, fseg_rows(p.a.seg_lo[k], p.a.seg_lo[k + 1]) * p.a.C);
-    const size_t lds = sizeof(float) * (size_t)fmax;
+        fmax = max(fmax, (fseg_rows(p.a.seg_lo[k], p.a.seg_lo[k + 1]) * p.a.C + 3) & ~3);
+    const size_t lds = sizeof(float) * ((size_t)fmax + (LV_STAGED_DEFAULT ? (size_t)kWavesPerBlock * stage_floats(LT, p.a.C) : 0));
     const dim3 grid(p.gx, p.gy), block(kThreads);
     const bool bf16 = p.dtype == LV_DTYPE_BF16;
     if (p.fused) {  // the fused path takes a shared spectrum (ActionNet's item_rep)

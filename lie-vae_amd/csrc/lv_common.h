@@ -50,6 +50,22 @@ __device__ __forceinline__ void store_out(__hip_bfloat16* p, float v) { *p = __f
 __device__ __forceinline__ float load_in(const float* p) { return *p; }
 __device__ __forceinline__ float load_in(const __hip_bfloat16* p) { return __bfloat162float(*p); }
 
+__device__ __forceinline__ void store_out2(float* p, float a, float b) {
+  *reinterpret_cast<float2*>(p) = make_float2(a, b);
+}
+__device__ __forceinline__ void store_out2(__hip_bfloat16* p, float a, float b) {
+  __hip_bfloat162 h;
+  h.x = __float2bfloat16(a);
+  h.y = __float2bfloat16(b);
+  *reinterpret_cast<__hip_bfloat162*>(p) = h;
+}
+
+// Exchange a value with the adjacent lane (0<->1, 2<->3, ...): DPP quad_perm [1,0,3,2].
+__device__ __forceinline__ float dpp_swap_adjacent(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 }  // namespace lv

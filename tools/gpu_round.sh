@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprof.  Every GPU step has its own
-# time limit; a fault/abort/timeout (exit >= 124 or signal) ends the script there.
+# One GPU-box session: parity tests, smoke, bench, rocprof (+ optional PMC / calibration).
+# Every GPU step has its own time limit; a fault/abort/timeout ends the script there.
+#   bash tools/gpu_round.sh [all|test|bench|prof]
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -24,8 +25,26 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --sweep
-  step bench_eager 600 python bench.py --launch eager --no-cpu-baseline
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline
+fi
+if [ "$MODE" = all ] || [ "$MODE" = train ]; then
+  step train_c3 600 python bench_train.py --global-batch 512 --steps 20
+fi
+if [ "$MODE" = prof ] || [ "$MODE" = traffic ]; then
+  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+  step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_tr/fetch" -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --launch eager --multistream 1
+  step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_tr/write" -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --launch eager --multistream 1
+  step traffic 60 python3 tools/pmc_traffic.py "$OUT/pmc_tr" "$OUT/traffic_B4096_L10_C10_f32.json"
+fi
+if [ "$MODE" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+  for g in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT"; do
+    tag=$(echo $g | cut -d' ' -f1)
+    step pmc_$tag 300 rocprofv3 --pmc $g --output-format csv -d "$OUT/pmc/$tag" -o run -- python3 bench.py --steps 100 --warmup 20 --no-cpu-baseline --launch eager
+  done
+  step pmc_summary 60 python3 tools/pmc_summary.py "$OUT/pmc" action_fwd
+  step storebench 120 ./tools/kbench_store 4096
 fi
 echo "=== done"

@@ -1,0 +1,31 @@
+"""HBM traffic per launch of the fused action kernel from rocprofv3 --pmc passes.
+
+Usage: python tools/pmc_traffic.py <pmc_root> <out.json>
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC EA requests).  Per
+MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of the bytes of wide (16 B/lane)
+coalesced streaming reads on gfx950 -- the kernel's reads (12 B/sample of v plus the
+4.8 KB spectrum per block) are narrow, so they are reported both raw and x2; WRITE_SIZE
+is exact for 16-B streaming stores (this kernel stores 8-B pairs, uncalibrated width).
+"""
+import csv
+import glob
+import json
+import sys
+
+root, out = sys.argv[1], sys.argv[2]
+vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+    for row in csv.DictReader(open(f)):
+        if "action_fwd" in row["Kernel_Name"] and row["Counter_Name"] in vals:
+            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+res = {}
+for k, v in vals.items():
+    if v:
+        v = sorted(v)[len(v) // 10:]  # drop the first-touch tail
+        res[k + "_kib_mean"] = sum(v) / len(v)
+fetch = res.get("FETCH_SIZE_kib_mean", 0.0) * 1024
+write = res.get("WRITE_SIZE_kib_mean", 0.0) * 1024
+res["hbm_bytes_per_launch"] = fetch + write
+res["hbm_bytes_per_launch_fetch_x2"] = 2 * fetch + write
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res))
