@@ -13,6 +13,9 @@ LV_EXTERN_LAUNCHERS(8) LV_EXTERN_LAUNCHERS(9) LV_EXTERN_LAUNCHERS(10) LV_EXTERN_
 LV_EXTERN_LAUNCHERS(12) LV_EXTERN_LAUNCHERS(13) LV_EXTERN_LAUNCHERS(14) LV_EXTERN_LAUNCHERS(15)
 LV_EXTERN_LAUNCHERS(16) LV_EXTERN_LAUNCHERS(17) LV_EXTERN_LAUNCHERS(18) LV_EXTERN_LAUNCHERS(19)
 LV_EXTERN_LAUNCHERS(20)
+LV_EXTERN_BWD(0) LV_EXTERN_BWD(1) LV_EXTERN_BWD(2) LV_EXTERN_BWD(3) LV_EXTERN_BWD(4)
+LV_EXTERN_BWD(5) LV_EXTERN_BWD(6) LV_EXTERN_BWD(7) LV_EXTERN_BWD(8) LV_EXTERN_BWD(9)
+LV_EXTERN_BWD(10) LV_EXTERN_BWD(11) LV_EXTERN_BWD(12) LV_EXTERN_BWD(13) LV_EXTERN_BWD(14)
 
 __global__ void action_bwd_reduce_kernel(const float* ws_ang, const float* ws_F, float* gang,
                                          float* gF, int64_t n, int64_t MC, int nseg, int gridX,
@@ -147,26 +150,28 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   return dispatch_L<FwdLauncher>(L, p);
 }
 
+// run-time index -> compile-time launcher tables
+template <template <int> class Launcher, class Args, int... Is>
+constexpr std::array<int (*)(Args&), sizeof...(Is)> launcher_table(std::integer_sequence<int, Is...>) {
+  return {&Launcher<Is>::run...};
+}
+constexpr auto kBwdRun = launcher_table<BwdLauncher, BwdLaunch>(std::make_integer_sequence<int, kNumBwdRanges>{});
+constexpr auto kWigRun = launcher_table<WigLauncher, WigLaunch>(std::make_integer_sequence<int, LV_MAX_DEGREE + 1>{});
+static_assert(bwd_range_hi(kNumBwdRanges - 1) == LV_MAX_DEGREE + 1, "backward ranges must cover l_max");
+
 struct BwdPlan {
-  int nseg, gx, groups, Sw;
-  int seg_lo[kMaxSeg + 1];
-  size_t lds, ws_ang, ws_F;
+  int nr, gx, groups, Sw;
+  size_t ws_ang, ws_F;
 };
 
 BwdPlan plan_bwd(int64_t n, int L, int C, bool sharedF) {
   BwdPlan b{};
   b.Sw = 64 / C;
-  b.nseg = choose_nseg(n, b.Sw, L, kPrologueFwd, true);
-  plan_segments(L, b.nseg, kPrologueFwd, true, b.seg_lo);
+  b.nr = bwd_num_ranges(L);
   b.groups = (int)((n + (int64_t)b.Sw * kWavesPerBlock - 1) / ((int64_t)b.Sw * kWavesPerBlock));
   // bound the slab count: each block walks several sample groups
   b.gx = std::max(1, std::min(b.groups, sharedF ? 512 : 1 << 30));
-  int max_seg_rows = 0;
-  for (int k = 0; k < b.nseg; ++k)
-    max_seg_rows = std::max(max_seg_rows, b.seg_lo[k + 1] * b.seg_lo[k + 1] - b.seg_lo[k] * b.seg_lo[k]);
-  const size_t wave_floats = 64 * (2 * L + 1) + 64 * 3 + (sharedF ? (size_t)max_seg_rows * C : 0);
-  b.lds = sizeof(float) * kWavesPerBlock * wave_floats;
-  b.ws_ang = sizeof(float) * (size_t)b.nseg * (size_t)n * 3;
+  b.ws_ang = sizeof(float) * (size_t)b.nr * (size_t)n * 3;
   const size_t MC = (size_t)(L + 1) * (L + 1) * C;
   b.ws_F = sharedF ? sizeof(float) * (size_t)b.gx * MC : 0;
   return b;
@@ -234,7 +239,6 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
   p.a.F = F;
   p.a.Fstride = F_batch_stride;
   p.a.gout = gout;
-  p.a.gang = gang;
   p.a.gF = gF;
   p.a.ws_ang = (float*)workspace;
   p.a.ws_F = (float*)((char*)workspace + b.ws_ang);
@@ -243,18 +247,19 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
   p.a.C = C;
   p.a.Sw = b.Sw;
   p.a.transpose = transpose ? 1 : 0;
-  p.a.nseg = b.nseg;
   p.a.groups = b.groups;
-  for (int k = 0; k <= kMaxSeg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
+  p.a.L = L;
   p.gx = b.gx;
-  p.gy = b.nseg;
-  p.lds = b.lds;
   p.stream = st;
-  LV_CHECK_ARG(b.lds <= 160 * 1024, "LDS plan too large (%zu B)", b.lds);
-  if (int e = dispatch_L<BwdLauncher>(L, p)) return e;
+  for (int r = 0; r < b.nr; ++r) {
+    const size_t lds = sizeof(float) * kWavesPerBlock * (size_t)bwd_wave_floats(r, L, C, sharedF);
+    LV_CHECK_ARG(lds <= 160 * 1024, "LDS plan too large (%zu B)", lds);
+    p.a.slot = r;
+    if (int e = kBwdRun[r](p)) return e;
+  }
   const int64_t work = std::max<int64_t>(n * 3, sharedF ? MC : 0);
   hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(work, 256)), dim3(256), 0, st,
-                     p.a.ws_ang, p.a.ws_F, gang, gF, n, MC, b.nseg, b.gx, sharedF ? 1 : 0);
+                     p.a.ws_ang, p.a.ws_F, gang, gF, n, MC, b.nr, b.gx, sharedF ? 1 : 0);
   LV_RETURN_LAUNCH("action_bwd_reduce_kernel");
 }
 
@@ -264,8 +269,10 @@ int lv_wigner_d_fwd(const float* ang, float* D, int64_t n, int L, void* stream) 
   LV_CHECK_ARG(L >= 0 && L <= LV_MAX_DEGREE, "l_max out of range");
   if (n == 0) return LV_OK;
   LV_CHECK_ARG(ang && D, "null pointer");
-  WigLaunch p{ang, D, n, (hipStream_t)stream};
-  return dispatch_L<WigLauncher>(L, p);
+  WigLaunch p{ang, D, n, (L + 1) * (2 * L + 1) * (2 * L + 3) / 3, (hipStream_t)stream};
+  for (int l = 0; l <= L; ++l)
+    if (int e = kWigRun[l](p)) return e;
+  return LV_OK;
 }
 
 }  // extern "C"

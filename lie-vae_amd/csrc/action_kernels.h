@@ -143,6 +143,72 @@ __device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], f
   dir(qr[0] * qr[3] + qr[1] * qr[2], qr[1] * qr[3] - qr[0] * qr[2], c1[2], s1[2]);
 }
 
+// General mean (z = mu @ exp(v)): the reference's op sequence (rodrigues, matmul, trace
+// method with its 1e-6 epsilon and first-argmax case, quaternion -> ZYZ) evaluated in
+// fp64 and rounded once to fp32 (cos, sin).  Near beta = 0 / pi the fp32 reference is
+// ill-conditioned (a 1-ulp change of z moves D by ~1e-5); fp64 keeps this path within
+// the reference's own fp64 evaluation.  Off the config-2 metric path (no mu there).
+__device__ __forceinline__ void mu_exp_to_zyz_trig(const float mu[9], const float vf[3],
+                                                   float c1[3], float s1[3], float qf[4]) {
+  const double v[3] = {vf[0], vf[1], vf[2]};
+  const double th = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  const double u[3] = {v[0] / th, v[1] / th, v[2] / th};
+  double sn, cs;
+  sincos(th, &sn, &cs);
+  const double omc = 1.0 - cs;
+  const double K[9] = {0, -u[2], u[1], u[2], 0, -u[0], -u[1], u[0], 0};
+  const double K2[9] = {-u[2] * u[2] - u[1] * u[1], u[1] * u[0], u[2] * u[0],
+                        u[0] * u[1], -u[2] * u[2] - u[0] * u[0], u[2] * u[1],
+                        u[0] * u[2], u[1] * u[2], -u[1] * u[1] - u[0] * u[0]};
+  double R[9], z[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + sn * K[i] + omc * K2[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      z[i * 3 + j] = (double)mu[i * 3] * R[j] + (double)mu[i * 3 + 1] * R[3 + j] +
+                     (double)mu[i * 3 + 2] * R[6 + j];
+  const double a = z[0], b = z[4], c = z[8];
+  const double pre[4] = {1 + a - b - c, 1 - a + b - c, 1 - a - b + c, 1 + a + b + c};
+  int k = 0;
+  double best = 0.5 * sqrt(1e-6 + fabs(pre[0]));
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    const double d = 0.5 * sqrt(1e-6 + fabs(pre[i]));
+    if (d > best) { best = d; k = i; }
+  }
+  const double s01 = z[1] + z[3], s02 = z[2] + z[6], s12 = z[5] + z[7];
+  const double d12 = z[5] - z[7], d20 = z[6] - z[2], d01 = z[1] - z[3];
+  const double r4 = 1.0 / (4.0 * best);
+  double q[4];
+  switch (k) {
+    case 0: q[0] = best; q[1] = s01 * r4; q[2] = s02 * r4; q[3] = d12 * r4; break;
+    case 1: q[0] = s01 * r4; q[1] = best; q[2] = s12 * r4; q[3] = d20 * r4; break;
+    case 2: q[0] = s02 * r4; q[1] = s12 * r4; q[2] = best; q[3] = d01 * r4; break;
+    default: q[0] = d12 * r4; q[1] = d20 * r4; q[2] = d01 * r4; q[3] = best; break;
+  }
+  double cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
+  cb = fmin(fmax(cb, (double)kEazyzLo), (double)kEazyzHi);
+  c1[1] = (float)cb;
+  s1[1] = (float)sqrt((1.0 - cb) * (1.0 + cb));
+  auto dir = [](double y, double x, float& cf, float& sf) {
+    const double r2 = x * x + y * y;
+    if (r2 == 0.0) {
+      cf = signbit(x) ? -1.f : 1.f;
+      sf = 0.f;
+    } else {
+      const double r = 1.0 / sqrt(r2);
+      cf = (float)(x * r);
+      sf = (float)(y * r);
+    }
+  };
+  dir(q[1] * q[2] - q[0] * q[3], q[0] * q[2] + q[1] * q[3], c1[0], s1[0]);
+  dir(q[0] * q[3] + q[1] * q[2], q[1] * q[3] - q[0] * q[2], c1[2], s1[2]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qf[i] = (float)q[i];
+}
+
 // Per-lane inputs, loaded before the block barrier so that their latency overlaps the
 // spectrum staging.
 struct LaneIn {
@@ -181,13 +247,7 @@ __device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& i
   if constexpr (FUSED) {
     float q[4];
     if (a.mu) {
-      // general mean: the reference's own fp32 sequence (exact division / sqrt, as the
-      // stand-alone conversion kernels), so the result tracks its rounding closely
-      float R[9], z[9];
-      rodrigues_fwd(in.v, R);
-      matmul3(in.mu, R, z);
-      mat_to_quat_fwd(z, q, nullptr);
-      quat_to_zyz_trig(q, cc, ss);
+      mu_exp_to_zyz_trig(in.mu, in.v, cc, ss, q);
     } else {
       exp_to_zyz_trig(in.v, cc, ss, q);
     }
@@ -451,25 +511,43 @@ struct ActionBwdArgs {
   const float* F;
   int64_t Fstride;
   const float* gout;
-  float* gang;         // final (n,3) (written by reduce kernel)
-  float* gF;           // final
-  float* ws_ang;       // [nseg][n][3]
+  float* gF;           // per-sample spectrum: written directly
+  float* ws_ang;       // [nranges][n][3]
   float* ws_F;         // [gridX][M*C] (shared F only)
   int64_t n;
   int64_t MC;
-  int C, Sw, transpose, nseg, groups;
-  int seg_lo[kMaxSeg + 1];
+  int C, Sw, transpose, groups, L, slot;
 };
 
-template <int LT>
+// Degree ranges of the backward, fixed at compile time and shared by every l_max:
+// [0,6) [6,8) then one degree per range up to 20.  Each range is its own kernel (small
+// functions: fast to compile, registers sized to the range), launched one after another;
+// the range containing l_max is clipped at run time.
+constexpr int kNumBwdRanges = 15;
+__host__ __device__ constexpr int bwd_range_lo(int r) { return r == 0 ? 0 : (r == 1 ? 6 : r + 6); }
+__host__ __device__ constexpr int bwd_range_hi(int r) { return r == 0 ? 6 : (r == 1 ? 8 : r + 7); }
+inline int bwd_num_ranges(int L) {
+  int n = 0;
+  while (n < kNumBwdRanges && bwd_range_lo(n) <= L) ++n;
+  return n;
+}
+inline int bwd_wave_floats(int r, int L, int C, bool sharedF) {
+  const int hi = bwd_range_hi(r) < L + 1 ? bwd_range_hi(r) : L + 1;
+  const int lo = bwd_range_lo(r);
+  const int LT = bwd_range_hi(r) - 1;
+  return 64 * (2 * LT + 1) + 64 * 3 + (sharedF ? (hi * hi - lo * lo) * C : 0);
+}
+
+template <int R>
 __global__ __launch_bounds__(kThreads) void action_bwd_kernel(ActionBwdArgs a) {
+  constexpr int LO = bwd_range_lo(R), HI = bwd_range_hi(R), LT = HI - 1;
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int C = a.C, Sw = a.Sw;
   const int j = lane / C;
   const int c = lane - j * C;
-  const int lo = a.seg_lo[blockIdx.y], hi = a.seg_lo[blockIdx.y + 1];
+  const int lo = LO, hi = min(HI, a.L + 1);
   const bool sharedF = a.Fstride == 0;
   const int rows_lo = lo * lo, rows_hi = hi * hi;
   const int seg_len = (rows_hi - rows_lo) * C;
@@ -504,9 +582,9 @@ __global__ __launch_bounds__(kThreads) void action_bwd_kernel(ActionBwdArgs a) {
     float ga = 0.f, gb = 0.f, gc = 0.f;
     const float* Fbase = a.F + (active ? s * a.Fstride : 0) + c;
 
-    sfor<LT + 1>([&](auto Lc) {
-      constexpr int l = LV_CV(Lc);
-      if (l >= lo && l < hi) {
+    sfor<HI - LO>([&](auto Lc) {
+      constexpr int l = LO + LV_CV(Lc);
+      if (l < hi) {
         constexpr int nn = 2 * l + 1;
         constexpr int r0 = l * l;
         const int rowlen = nn * C;
@@ -592,7 +670,7 @@ __global__ __launch_bounds__(kThreads) void action_bwd_kernel(ActionBwdArgs a) {
       float r[3] = {0.f, 0.f, 0.f};
       for (int cc2 = 0; cc2 < C; ++cc2)
         for (int i = 0; i < 3; ++i) r[i] += apart[(lane + cc2) * 3 + i];
-      float* dst = a.ws_ang + ((int64_t)blockIdx.y * a.n + s) * 3;
+      float* dst = a.ws_ang + ((int64_t)a.slot * a.n + s) * 3;
       dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2];
     }
     wave_lds_sync();
@@ -611,35 +689,28 @@ __global__ __launch_bounds__(kThreads) void action_bwd_kernel(ActionBwdArgs a) {
 }
 
 // ------------------------------------------------------------ Wigner-D blocks
-// Column q of D_l = chain applied to e_q; one thread per (sample, l, q).
-template <int LT>
-__global__ void wigner_d_kernel(const float* ang, float* D, int64_t n) {
-  constexpr int cols = (LT + 1) * (LT + 1);  // sum_l (2l+1)
+// Column q of D_l = chain applied to e_q; one thread per (sample, q), one kernel per
+// degree.  D is (n, dsz) with block l row-major at offset off.
+template <int l>
+__global__ void wigner_d_kernel(const float* ang, float* D, int64_t n, int dsz) {
+  constexpr int nn = 2 * l + 1;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= n * cols) return;
-  const int64_t s = tid / cols;
-  const int col = (int)(tid - s * cols);
+  if (tid >= n * nn) return;
+  const int64_t s = tid / nn;
+  const int q = (int)(tid - s * nn);
   float c1[3], s1[3];
   for (int i = 0; i < 3; ++i) sincosf(ang[s * 3 + i], &s1[i], &c1[i]);
-  TrigTab<LT> t;
-  trig_fill<LT>(t, c1, s1, LT);
-  constexpr int dsz = (LT + 1) * (2 * LT + 1) * (2 * LT + 3) / 3;
-  sfor<LT + 1>([&](auto Lc) {
-    constexpr int l = LV_CV(Lc);
-    constexpr int nn = 2 * l + 1;
-    if (col >= l * l && col < (l + 1) * (l + 1)) {
-      const int q = col - l * l;
-      float x[nn], y[nn];
-      sfor<nn>([&](auto K) { x[LV_CV(K)] = (LV_CV(K) == q) ? 1.f : 0.f; });
-      xrot<l, 2>(t, x, y);
-      jmul<l>(y, x);
-      xrot<l, 1>(t, x, y);
-      jmul<l>(y, x);
-      xrot<l, 0>(t, x, y);
-      constexpr int off = l * (2 * l - 1) * (2 * l + 1) / 3;  // sum_{k<l} (2k+1)^2
-      sfor<nn>([&](auto I) { D[s * dsz + off + LV_CV(I) * nn + q] = y[LV_CV(I)]; });
-    }
-  });
+  TrigTab<l> t;
+  trig_fill<l>(t, c1, s1, l);
+  float x[nn], y[nn];
+  sfor<nn>([&](auto K) { x[LV_CV(K)] = (LV_CV(K) == q) ? 1.f : 0.f; });
+  xrot<l, 2>(t, x, y);
+  jmul<l>(y, x);
+  xrot<l, 1>(t, x, y);
+  jmul<l>(y, x);
+  xrot<l, 0>(t, x, y);
+  constexpr int off = l * (2 * l - 1) * (2 * l + 1) / 3;  // sum_{k<l} (2k+1)^2
+  sfor<nn>([&](auto I) { D[s * dsz + off + LV_CV(I) * nn + q] = y[LV_CV(I)]; });
 }
 
 // ------------------------------------------------------------------ host side
@@ -687,16 +758,16 @@ struct FwdLauncher {
 
 struct BwdLaunch {
   ActionBwdArgs a;
-  int gx, gy;
-  size_t lds;
+  int gx;
   hipStream_t stream;
 };
 
-template <int LT>
+template <int R>
 struct BwdLauncher {
-  using Args = BwdLaunch;
   static int run(BwdLaunch& p) {
-    hipLaunchKernelGGL((action_bwd_kernel<LT>), dim3(p.gx, p.gy), dim3(kThreads), p.lds, p.stream, p.a);
+    const size_t lds = sizeof(float) * kWavesPerBlock *
+                       (size_t)bwd_wave_floats(R, p.a.L, p.a.C, p.a.Fstride == 0);
+    hipLaunchKernelGGL((action_bwd_kernel<R>), dim3(p.gx), dim3(kThreads), lds, p.stream, p.a);
     LV_RETURN_LAUNCH("action_bwd_kernel");
   }
 };
@@ -705,23 +776,23 @@ struct WigLaunch {
   const float* ang;
   float* D;
   int64_t n;
+  int dsz;
   hipStream_t stream;
 };
 
-template <int LT>
+template <int l>
 struct WigLauncher {
-  using Args = WigLaunch;
   static int run(WigLaunch& p) {
-    const int64_t total = p.n * (int64_t)(LT + 1) * (LT + 1);
-    hipLaunchKernelGGL((wigner_d_kernel<LT>), dim3(ceil_div(total, 256)), dim3(256), 0, p.stream,
-                       p.ang, p.D, p.n);
+    const int64_t total = p.n * (2 * l + 1);
+    hipLaunchKernelGGL((wigner_d_kernel<l>), dim3(ceil_div(total, 256)), dim3(256), 0, p.stream,
+                       p.ang, p.D, p.n, p.dsz);
     LV_RETURN_LAUNCH("wigner_d_kernel");
   }
 };
 
 #define LV_EXTERN_LAUNCHERS(L)            \
   extern template struct FwdLauncher<L>;  \
-  extern template struct BwdLauncher<L>;  \
   extern template struct WigLauncher<L>;
+#define LV_EXTERN_BWD(R) extern template struct BwdLauncher<R>;
 
 }  // namespace lv

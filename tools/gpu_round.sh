@@ -25,11 +25,16 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --sweep
+  step bench_c5 600 python bench.py --lmax 20 --batch 8192 --dtype bf16 --no-cpu-baseline --steps 500
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline --multistream 1
+  rm -f "$OUT"/prof/*kernel_trace.csv
 fi
 if [ "$MODE" = all ] || [ "$MODE" = train ]; then
   step train_c3 600 python bench_train.py --global-batch 512 --steps 20
+  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+  step prof_train 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o run --output-format csv -- python3 bench_train.py --steps 10 --warmup 3
+  rm -f "$OUT"/prof_train/*kernel_trace.csv
 fi
 if [ "$MODE" = prof ] || [ "$MODE" = traffic ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
