@@ -1,6 +1,8 @@
 // Host side of the group-action kernels: degree-range planning (segments), launch
 // geometry, argument checks and the extern "C" entry points of include/lievae.h.
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <array>
 #include <vector>
 
@@ -93,6 +95,49 @@ inline int choose_nseg(int64_t n, int Sw, int L, double P, bool bwd) {
 constexpr double kPrologueFwd = 200.0;
 constexpr double kPrologueFused = 250.0;
 
+// Tile kernel (shared spectrum): one block per sample group, one wave per degree
+// segment, output staged in LDS and written as whole lines.  Measured on MI355X
+// (tools/tilebench.hip, l = 10, C = 10): 5 segments best at batch 4096, 4 at 65536;
+// write-through (sc1) stores best while the output is small enough to be written during
+// the kernel (batch 4096, 19.8 MB: 7.4 vs 8.3 us nt), nt beyond (65536: 77 vs 93 us).
+constexpr size_t kTileMaxLds = 64 * 1024;  // >= 2 blocks per CU (l = 20 bf16 ran 53 vs 43 us at 85 KB)
+constexpr double kTileSegCostSmall = 450.0;   // per-wave chain cost target, few groups
+constexpr double kTileSegCostLarge = 560.0;   // ... many groups (>= kTileManyGroups)
+constexpr int64_t kTileManyGroups = 2048;
+constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
+
+// LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy (A/B
+// testing and diagnosis only; read once per process).
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
+  static const int kEnvTile = env_int("LV_TILE", 1);
+  static const int kEnvWT = env_int("LV_TILE_WT", -1);
+  if (!kEnvTile) return false;
+  ActionArgs& a = p.a;
+  const int64_t groups = (a.n + a.Sw - 1) / a.Sw;
+  double total = 0.0;
+  for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
+  const double target = groups < kTileManyGroups ? kTileSegCostSmall : kTileSegCostLarge;
+  const int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
+  plan_segments(L, nseg, kPrologueFused, false, a.seg_lo);
+  int fp = 0;
+  for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
+  a.fpitch = (fp + 3) & ~3;
+  const size_t lds = (size_t)tile_stage_bytes(a.Sw, a.MC, out_bytes) + sizeof(float) * nseg * a.fpitch;
+  if (lds > kTileMaxLds || groups > 0x7fffffff) return false;
+  a.write_through = (int64_t)a.n * a.MC * out_bytes <= kWriteThroughMaxBytes ? 1 : 0;
+  if (kEnvWT >= 0) a.write_through = kEnvWT;
+  p.tile = true;
+  p.lds = lds;
+  p.gx = (int)groups;
+  p.gy = nseg;
+  return true;
+}
+
 template <template <int> class Launcher, int LT = 0>
 int dispatch_L(int L, typename Launcher<0>::Args& args) {
   if constexpr (LT > LV_MAX_DEGREE) {
@@ -137,6 +182,11 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   p.a.C = C;
   p.a.Sw = 64 / C;
   p.a.transpose = transpose ? 1 : 0;
+  p.fused = fused;
+  p.dtype = out_dtype;
+  p.stream = stream;
+  if (Fstride == 0 && plan_tile(p, L, out_dtype == LV_DTYPE_BF16 ? 2 : 4))
+    return dispatch_L<FwdLauncher>(L, p);
   const double P = fused ? kPrologueFused : kPrologueFwd;
   const int nseg = choose_nseg(n, p.a.Sw, L, P, false);
   plan_segments(L, nseg, P, false, p.a.seg_lo);

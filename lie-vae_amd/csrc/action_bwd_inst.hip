@@ -1,6 +1,6 @@
 // Explicit instantiation of one backward degree-range kernel (LV_BWD_R in
 // [0, kNumBwdRanges)), one object per range.
-#include "action_kernels.h"
+#include "action_bwd.h"
 
 #ifndef LV_BWD_R
 #error "compile with -DLV_BWD_R=<range>"

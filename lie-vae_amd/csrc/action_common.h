@@ -1,0 +1,276 @@
+#pragma once
+// Shared pieces of the group-action kernels for gfx950 (MI355X): launch arguments, the
+// fused prologue maths (z = mu·exp(v) -> ZYZ (cos, sin)) and per-lane input staging.
+// Forward kernels: action_fwd.h; backward: action_bwd.h; host planning: action.hip.
+#include "action_chain.h"
+#include "so3_device.h"
+
+// Diagnostic timestamps (tools/kbench.hip builds with -DLV_STAMPS; never in the library).
+#ifndef LV_STORE_MODE
+#define LV_STORE_MODE 0
+#endif
+#ifndef LV_PROLOGUE_MODE
+#define LV_PROLOGUE_MODE 0
+#endif
+#ifndef LV_TILE_DIAG
+#define LV_TILE_DIAG 0
+#endif
+#ifdef LV_STAMPS
+__device__ unsigned long long* lv_stamp_buf;
+#define LV_STAMP(slot)                                                                  \
+  do {                                                                                  \
+    if ((threadIdx.x & 63) == 0) {                                                      \
+      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                   \
+      const unsigned long long w_ = ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * \
+                                    (blockDim.x >> 6) + (threadIdx.x >> 6);             \
+      lv_stamp_buf[w_ * 8 + (slot)] = t_;                                               \
+    }                                                                                   \
+  } while (0)
+#else
+#define LV_STAMP(slot) do {} while (0)
+#endif
+
+namespace lv {
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kThreads = 64 * kWavesPerBlock;
+constexpr int kMaxSeg = 16;
+
+struct ActionArgs {
+  const float* ang;     // (n,3) angles (non-fused)
+  const float* mu;      // (n,3,3) or null (fused)
+  const float* v;       // (n,3) algebra vector (fused)
+  const float* F;       // spectrum
+  int64_t Fstride;      // 0 (shared) or M*C
+  void* out;            // (n,M,C)
+  float* ang_out;       // optional (fused)
+  int64_t n;
+  int64_t MC;
+  int C, Sw, transpose;
+  int fpitch;           // tile kernel: floats per wave-private spectrum slice in LDS
+  int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores
+  int seg_lo[kMaxSeg + 1];
+};
+
+// ---- fused-prologue maths (per lane, registers).
+
+// ZYZ (cos, sin) straight from the quaternion: the function quaternions_to_eazyz
+// (lie_tools.py:160-175) followed by cos/sin.  atan2(y, x) -> (x, y)/|(x, y)| with the
+// atan2(+-0, +-0) edge mirrored; acos(clamp(w)) -> (w, sqrt((1-w)(1+w))).
+__device__ __forceinline__ void quat_to_zyz_trig(const float q[4], float c1[3], float s1[3]) {
+  const float a1 = q[1] * q[2] - q[0] * q[3];
+  const float b1 = q[0] * q[2] + q[1] * q[3];
+  const float cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
+  const float a3 = q[0] * q[3] + q[1] * q[2];
+  const float b3 = q[1] * q[3] - q[0] * q[2];
+  auto dir = [](float y, float x, float& c, float& s) {
+    const float r2 = x * x + y * y;
+    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
+      c = signbit(x) ? -1.f : 1.f;
+      s = 0.f;
+    } else {
+      const float r = rsqrtf(r2);
+      c = x * r;
+      s = y * r;
+    }
+  };
+  dir(a1, b1, c1[0], s1[0]);
+  const float x = fminf(fmaxf(cb, kEazyzLo), kEazyzHi);
+  c1[1] = x;
+  s1[1] = sqrtf((1.f - x) * (1.f + x));
+  dir(a3, b3, c1[2], s1[2]);
+}
+
+// The same (cos, sin) for z = exp(v) straight from the axis-angle form, at better than
+// fp32-reference accuracy.  The reference's q = group_matrix_to_quaternions(rodrigues(v))
+// is, in exact arithmetic, the unit quaternion q* = (-u sin(t/2), cos(t/2)) of R(v) (its
+// matrix is the transpose of the active one) with the trace method's epsilon applied to
+// the largest component k: q_k -> d = sqrt(q_k^2 + 2.5e-7), q_j -> sign(q_k) q_j |q_k| / d
+// (lie_tools.py:126-156).  cos(beta) = 1 - (1 - cb) is formed in "one-minus" form so that
+// sin(beta) = sqrt((1-cb)(1+cb)) keeps full relative accuracy near beta = 0 / pi, where the
+// reference's fp32 acos(cb) loses it (the clamp to +-(1 - 1e-6) is mirrored exactly).
+__device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], float s1[3],
+                                                float qr[4]) {
+  const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const float inv = rsqrtf(vv);  // NaN downstream at v = 0, as the reference
+  const float th = vv * inv;
+  float sh, ch;
+  sincosf(0.5f * th, &sh, &ch);
+  const float m = -sh * inv;
+  const float qt[4] = {v[0] * m, v[1] * m, v[2] * m, ch};
+  int k = 0;
+  float best = fabsf(qt[0]);
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (fabsf(qt[i]) > best) { best = fabsf(qt[i]); k = i; }
+  const float qk = k == 0 ? qt[0] : (k == 1 ? qt[1] : (k == 2 ? qt[2] : qt[3]));
+  constexpr float eps = 2.5e-7f;
+  const float qk2 = qk * qk;
+  const float d = sqrtf(qk2 + eps);
+  const float sc = copysignf(best / d, qk);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
+  const float oms = eps * (1.f - 2.f * qk2 - eps) / (qk2 + eps);  // 1 - |q_ref|^2
+  float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
+  float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
+  constexpr float kDelta = 1.f - kEazyzHi;                          // exact in fp32
+  if (omc < kDelta) { omc = kDelta; opc = 2.f - kDelta; }
+  else if (opc < kDelta) { opc = kDelta; omc = 2.f - kDelta; }
+  c1[1] = omc <= opc ? 1.f - omc : opc - 1.f;
+  s1[1] = sqrtf(omc * opc);
+  auto dir = [](float y, float x, float& c, float& s) {
+    const float r2 = x * x + y * y;
+    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
+      c = signbit(x) ? -1.f : 1.f;
+      s = 0.f;
+    } else {
+      const float r = rsqrtf(r2);
+      c = x * r;
+      s = y * r;
+    }
+  };
+  dir(qr[1] * qr[2] - qr[0] * qr[3], qr[0] * qr[2] + qr[1] * qr[3], c1[0], s1[0]);
+  dir(qr[0] * qr[3] + qr[1] * qr[2], qr[1] * qr[3] - qr[0] * qr[2], c1[2], s1[2]);
+}
+
+// General mean (z = mu @ exp(v)): the reference's op sequence (rodrigues, matmul, trace
+// method with its 1e-6 epsilon and first-argmax case, quaternion -> ZYZ) evaluated in
+// fp64 and rounded once to fp32 (cos, sin).  Near beta = 0 / pi the fp32 reference is
+// ill-conditioned (a 1-ulp change of z moves D by ~1e-5); fp64 keeps this path within
+// the reference's own fp64 evaluation.  Off the config-2 metric path (no mu there).
+__device__ __forceinline__ void mu_exp_to_zyz_trig(const float mu[9], const float vf[3],
+                                                   float c1[3], float s1[3], float qf[4]) {
+  const double v[3] = {vf[0], vf[1], vf[2]};
+  const double th = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  const double u[3] = {v[0] / th, v[1] / th, v[2] / th};
+  double sn, cs;
+  sincos(th, &sn, &cs);
+  const double omc = 1.0 - cs;
+  const double K[9] = {0, -u[2], u[1], u[2], 0, -u[0], -u[1], u[0], 0};
+  const double K2[9] = {-u[2] * u[2] - u[1] * u[1], u[1] * u[0], u[2] * u[0],
+                        u[0] * u[1], -u[2] * u[2] - u[0] * u[0], u[2] * u[1],
+                        u[0] * u[2], u[1] * u[2], -u[1] * u[1] - u[0] * u[0]};
+  double R[9], z[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + sn * K[i] + omc * K2[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      z[i * 3 + j] = (double)mu[i * 3] * R[j] + (double)mu[i * 3 + 1] * R[3 + j] +
+                     (double)mu[i * 3 + 2] * R[6 + j];
+  const double a = z[0], b = z[4], c = z[8];
+  const double pre[4] = {1 + a - b - c, 1 - a + b - c, 1 - a - b + c, 1 + a + b + c};
+  int k = 0;
+  double best = 0.5 * sqrt(1e-6 + fabs(pre[0]));
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    const double d = 0.5 * sqrt(1e-6 + fabs(pre[i]));
+    if (d > best) { best = d; k = i; }
+  }
+  const double s01 = z[1] + z[3], s02 = z[2] + z[6], s12 = z[5] + z[7];
+  const double d12 = z[5] - z[7], d20 = z[6] - z[2], d01 = z[1] - z[3];
+  const double r4 = 1.0 / (4.0 * best);
+  double q[4];
+  switch (k) {
+    case 0: q[0] = best; q[1] = s01 * r4; q[2] = s02 * r4; q[3] = d12 * r4; break;
+    case 1: q[0] = s01 * r4; q[1] = best; q[2] = s12 * r4; q[3] = d20 * r4; break;
+    case 2: q[0] = s02 * r4; q[1] = s12 * r4; q[2] = best; q[3] = d01 * r4; break;
+    default: q[0] = d12 * r4; q[1] = d20 * r4; q[2] = d01 * r4; q[3] = best; break;
+  }
+  double cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
+  cb = fmin(fmax(cb, (double)kEazyzLo), (double)kEazyzHi);
+  c1[1] = (float)cb;
+  s1[1] = (float)sqrt((1.0 - cb) * (1.0 + cb));
+  auto dir = [](double y, double x, float& cf, float& sf) {
+    const double r2 = x * x + y * y;
+    if (r2 == 0.0) {
+      cf = signbit(x) ? -1.f : 1.f;
+      sf = 0.f;
+    } else {
+      const double r = 1.0 / sqrt(r2);
+      cf = (float)(x * r);
+      sf = (float)(y * r);
+    }
+  };
+  dir(q[1] * q[2] - q[0] * q[3], q[0] * q[2] + q[1] * q[3], c1[0], s1[0]);
+  dir(q[0] * q[3] + q[1] * q[2], q[1] * q[3] - q[0] * q[2], c1[2], s1[2]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qf[i] = (float)q[i];
+}
+
+// Per-lane inputs, loaded before the block barrier so that their latency overlaps the
+// spectrum staging.
+struct LaneIn {
+  float v[3];
+  float mu[9];
+};
+
+template <bool FUSED>
+__device__ __forceinline__ void lane_load(const ActionArgs& a, int64_t s, LaneIn& in) {
+  if constexpr (FUSED) {
+#if LV_PROLOGUE_MODE == 2  // diagnostic: no input load (synthetic v from the index)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in.v[i] = 0.3f + 0.001f * (float)((s * 3 + i) & 1023);
+    return;
+#endif
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in.v[i] = a.v[s * 3 + i];
+    if (a.mu) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) in.mu[i] = a.mu[s * 9 + i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in.v[i] = a.ang[s * 3 + i];
+  }
+}
+
+// (cos, sin) of the three chain angles.  For transpose (D^T = X(-c) J X(-b) J X(-a)) the
+// slots are swapped and the sines negated.
+template <bool FUSED>
+__device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& in, int64_t s,
+                                            bool active, int c, bool write_ang, float c1[3],
+                                            float s1[3]) {
+  float cc[3], ss[3];
+#if LV_PROLOGUE_MODE == 1  // diagnostic: trivial angles (loads kept)
+  if (true) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { cc[i] = in.v[i]; ss[i] = in.v[(i + 1) % 3]; }
+  } else
+#endif
+  if constexpr (FUSED) {
+    float q[4];
+    if (a.mu) {
+      mu_exp_to_zyz_trig(in.mu, in.v, cc, ss, q);
+    } else {
+      exp_to_zyz_trig(in.v, cc, ss, q);
+    }
+    if (write_ang && active && c == 0) {
+      float ang[3];
+      quat_to_eazyz_fwd(q, ang);
+      a.ang_out[s * 3 + 0] = ang[0];
+      a.ang_out[s * 3 + 1] = ang[1];
+      a.ang_out[s * 3 + 2] = ang[2];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sincosf(in.v[i], &ss[i], &cc[i]);
+  }
+  if (a.transpose) {
+    c1[0] = cc[2]; s1[0] = -ss[2];
+    c1[1] = cc[1]; s1[1] = -ss[1];
+    c1[2] = cc[0]; s1[2] = -ss[0];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { c1[i] = cc[i]; s1[i] = ss[i]; }
+  }
+}
+
+// Rows of a degree segment's spectrum slice as staged in LDS, column-major
+// ([c][row]) so that a lane's column is contiguous (immediate LDS offsets) and padded
+// to an odd count so that the C columns fall in different banks.
+__host__ __device__ inline int fseg_rows(int lo, int hi) { return (hi * hi - lo * lo) | 1; }
+
+
+}  // namespace lv
