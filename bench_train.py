@@ -24,6 +24,7 @@ import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lie-vae_amd"))
+F32_PEAK_TFLOPS = 157.3  # MI355X f32 MFMA = f32 VALU (v_pk_fma_f32) peak, MI355X_MICROARCH.md
 
 
 def main():
@@ -35,7 +36,11 @@ def main():
     ap.add_argument("--deconv-hidden", type=int, default=200)
     ap.add_argument("--mean-mode", default="s2s2")
     ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--no-find", dest="find", action="store_false",
+                    help="keep MIOpen's heuristic conv solutions (default: torch.backends."
+                         "cudnn.benchmark, MIOpen times the candidates once per shape)")
     args = ap.parse_args()
+    torch.backends.cudnn.benchmark = args.find
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -63,6 +68,12 @@ def main():
 
     for _ in range(args.warmup):
         trainer.step(x)
+    # model FLOPs of one step (forward + backward, counted per aten op: the convs,
+    # deconvs and linear layers; the SO(3) kernels are custom ops and not counted)
+    from torch.utils.flop_counter import FlopCounterMode
+    with FlopCounterMode(display=False) as fc:
+        trainer.step(x)
+    step_flops = fc.get_total_flops()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -85,7 +96,12 @@ def main():
             "steps": args.steps, "ms_per_step": el * 1e3 / args.steps,
             "config": {"global_batch": args.global_batch, "per_gpu": B, "l_max": args.lmax,
                        "deconv_hidden": args.deconv_hidden, "mean_mode": args.mean_mode,
-                       "params": param_count(model), "dtype": "f32"},
+                       "params": param_count(model), "dtype": "f32",
+                       "channels_last": args.channels_last, "miopen_find": args.find},
+            "matrix": {"flops_per_step_per_gpu": step_flops,
+                       "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,
+                       "peak_tflops": F32_PEAK_TFLOPS,
+                       "frac": step_flops / (el / args.steps) / 1e12 / F32_PEAK_TFLOPS},
             "loss": float(loss.item()), "recon": float(recon.mean().item()),
             "kl": float(kl.mean().item())}), flush=True)
     if world > 1:

@@ -68,6 +68,62 @@ __device__ __forceinline__ void xrot(const TrigTab<LT>& t, const float (&x)[2 * 
   });
 }
 
+// The same multiples kept in LDS instead of registers (large l: the register table is
+// 6(l+1) VGPRs and caps occupancy at 2 waves per SIMD at l = 20).  Row of one sample:
+// [2A][f] = cos(f θ_A), [2A+1][f] = sin(f θ_A), f = 0..TP-1; kTrigRow floats per sample
+// (padded so the samples of a wave fall in different LDS banks).
+template <int LT>
+struct TrigLds {
+  static constexpr int TP = (LT + 1 + 3) & ~3;
+  static constexpr int kRow = 6 * TP + 4;
+};
+
+// Write slot q's multiples f = 0..upto (trig_fill's recurrence, same rounding).
+template <int LT>
+__device__ __forceinline__ void trig_row_fill(float* tj, const float c1[3], const float s1[3],
+                                              int q, int upto) {
+  constexpr int TP = TrigLds<LT>::TP;
+  const float cq = q == 0 ? c1[0] : (q == 1 ? c1[1] : c1[2]);
+  const float sq = q == 0 ? s1[0] : (q == 1 ? s1[1] : s1[2]);
+  float* tc = tj + 2 * q * TP;
+  float* ts = tc + TP;
+  tc[0] = 1.f;
+  ts[0] = 0.f;
+  float cf = cq, sf = sq;
+  sfor<LT + 1>([&](auto F) {
+    constexpr int f = LV_CV(F);
+    if constexpr (f >= 1) {
+      if (f <= upto) {
+        if constexpr (f >= 2) {
+          const float cn = fmaf(cf, cq, -(sf * sq));
+          sf = fmaf(sf, cq, cf * sq);
+          cf = cn;
+        }
+        tc[f] = cf;
+        ts[f] = sf;
+      }
+    }
+  });
+}
+
+// y = X_l(θ_A) x with the multiples read from an LDS row (bitwise equal to xrot).
+template <int l, int A, int LT>
+__device__ __forceinline__ void xrot_lds(const float* tj, const float (&x)[2 * l + 1],
+                                         float (&y)[2 * l + 1]) {
+  constexpr int TP = TrigLds<LT>::TP;
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) {
+      y[i] = x[i];
+    } else if constexpr (f > 0) {
+      y[i] = fmaf(tj[2 * A * TP + f], x[i], tj[(2 * A + 1) * TP + f] * x[2 * l - i]);
+    } else {
+      y[i] = fmaf(tj[2 * A * TP - f], x[i], -(tj[(2 * A + 1) * TP - f] * x[2 * l - i]));
+    }
+  });
+}
+
 // y = X_l(θ_A)^T x = X_l(-θ_A) x
 template <int l, int A, int LT>
 __device__ __forceinline__ void xrot_t(const TrigTab<LT>& t, const float (&x)[2 * l + 1],

@@ -35,6 +35,7 @@ namespace lv {
 constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = 64 * kWavesPerBlock;
 constexpr int kMaxSeg = 16;
+constexpr int kTrigLdsMinL = 13;  // action_fwd_kernel keeps the trig table in LDS from here
 
 struct ActionArgs {
   const float* ang;     // (n,3) angles (non-fused)

@@ -119,12 +119,25 @@ __global__ __launch_bounds__(kThreads) void action_fwd_kernel(ActionArgs a) {
       fv[k] = e < fcnt ? fsrc[e] : 0.f;
     }
   }
+  // l >= kTrigLdsMinL: the per-sample (cos, sin) multiples live in a wave-private LDS table
+  // (one row per sample, written by the sample's first three lanes) instead of 6(l+1)
+  // VGPRs per lane -- 202 -> ~120 VGPRs at l = 20, i.e. 4 instead of 2 waves per SIMD.
+  constexpr bool TL = LT >= kTrigLdsMinL && !STAGED;
+  constexpr int kRow = TrigLds<LT>::kRow;
+  float* trow = lds + a.fpitch + wave * Sw * kRow;
   float c1[3], s1[3];
-  TrigTab<LT> t;
+  TrigTab<TL ? 0 : LT> t;
   if (Sv > 0) {
     lane_angles<FUSED>(a, in, s, active, c, FUSED && a.ang_out && blockIdx.y == 0, c1, s1);
-    trig_fill<LT>(t, c1, s1, hi - 1);
+    if constexpr (TL) {
+      if (j < Sw)
+        for (int q = c; q < 3; q += C) trig_row_fill<LT>(trow + j * kRow, c1, s1, q, hi - 1);
+      if constexpr (!SHARED) wave_lds_sync();
+    } else {
+      trig_fill<LT>(t, c1, s1, hi - 1);
+    }
   }
+  const float* tj = trow + min(j, Sw - 1) * kRow;
   LV_STAMP(1);
   if constexpr (SHARED) {
 #pragma unroll
@@ -177,11 +190,19 @@ __global__ __launch_bounds__(kThreads) void action_fwd_kernel(ActionArgs a) {
 #pragma unroll
       for (int i = 0; i < nn; ++i) y[i] = x[i] * c1[0];
 #else
-      xrot<l, 2>(t, x, y);
-      jmul<l>(y, x);
-      xrot<l, 1>(t, x, y);
-      jmul<l>(y, x);
-      xrot<l, 0>(t, x, y);
+      if constexpr (TL) {
+        xrot_lds<l, 2, LT>(tj, x, y);
+        jmul<l>(y, x);
+        xrot_lds<l, 1, LT>(tj, x, y);
+        jmul<l>(y, x);
+        xrot_lds<l, 0, LT>(tj, x, y);
+      } else {
+        xrot<l, 2>(t, x, y);
+        jmul<l>(y, x);
+        xrot<l, 1>(t, x, y);
+        jmul<l>(y, x);
+        xrot<l, 0>(t, x, y);
+      }
 #endif
 #if LV_STORE_MODE == 1  // diagnostic: no stores, outputs kept live
 #pragma unroll
@@ -291,35 +312,52 @@ __host__ __device__ inline int tile_stage_bytes(int Sw, int64_t MC, int out_byte
 // body (ds_read_b128 -> buffer_store_dwordx4, 1 KiB per wave instruction), tail elements.
 // The LDS tile starts `mis` bytes past a 16-B boundary, mis = gout mod 16, so LDS and
 // global addresses agree mod 16.
+// Threads tid = 0..nthr-1 of the block take part.
 template <typename OutT, int POL>
-__device__ __forceinline__ void tile_flush(OutT* gout, const char* stage_b, int mis, int nbytes) {
+__device__ __forceinline__ void tile_flush(OutT* gout, const char* stage_b, int mis, int nbytes,
+                                           int tid, int nthr) {
   const int head = min((16 - mis) & 15, nbytes);
   const int nvec = (nbytes - head) >> 4;
   const int tail0 = head + nvec * 16;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(gout, 0, nbytes, kRawBufferFlags);
-  const int nthr = blockDim.x;
-  for (int k = threadIdx.x; k < nvec; k += nthr) {
+  for (int k = tid; k < nvec; k += nthr) {
     const lv_f4 v = *reinterpret_cast<const lv_f4*>(stage_b + head + 16 * k);
     tile_store16<POL>(rs, head + 16 * k, v);
   }
   constexpr int E = (int)sizeof(OutT);
   const int nedge = head / E + (nbytes - tail0) / E;
-  if ((int)threadIdx.x < nedge) {
-    const int b = (int)threadIdx.x < head / E ? (int)threadIdx.x * E
-                                              : tail0 + ((int)threadIdx.x - head / E) * E;
+  if (tid < nedge) {
+    const int b = tid < head / E ? tid * E : tail0 + (tid - head / E) * E;
     tile_store_elem<POL>(rs, b, *reinterpret_cast<const OutT*>(stage_b + b));
   }
+}
+template <typename OutT, int POL>
+__device__ __forceinline__ void tile_flush(OutT* gout, const char* stage_b, int mis, int nbytes) {
+  tile_flush<OutT, POL>(gout, stage_b, mis, nbytes, (int)threadIdx.x, (int)blockDim.x);
+}
+
+// Block barrier for LDS hand-offs only: waits for this wave's LDS operations, never for
+// its global stores (a __syncthreads() release fence may emit s_waitcnt vmcnt(0) and
+// stall on the previous tile's stores still in flight).
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // The store policy picked at run time (uniform branch; aux bits must be immediates).
 template <typename OutT>
 __device__ __forceinline__ void tile_flush_rt(OutT* gout, const char* stage_b, int mis, int nbytes,
-                                              int write_through) {
+                                              int write_through, int tid, int nthr) {
   if (write_through)
-    tile_flush<OutT, 16>(gout, stage_b, mis, nbytes);
+    tile_flush<OutT, 16>(gout, stage_b, mis, nbytes, tid, nthr);
   else
-    tile_flush<OutT, 1>(gout, stage_b, mis, nbytes);
+    tile_flush<OutT, 1>(gout, stage_b, mis, nbytes, tid, nthr);
+}
+template <typename OutT>
+__device__ __forceinline__ void tile_flush_rt(OutT* gout, const char* stage_b, int mis, int nbytes,
+                                              int write_through) {
+  tile_flush_rt<OutT>(gout, stage_b, mis, nbytes, write_through, (int)threadIdx.x,
+                      (int)blockDim.x);
 }
 
 template <int LT, bool FUSED, typename OutT, int POL, bool WAVEFLUSH = false>
@@ -502,7 +540,10 @@ struct FwdLauncher {
     if (shared)
       for (int k = 0; k < p.gy; ++k)
         fmax = max(fmax, (fseg_rows(p.a.seg_lo[k], p.a.seg_lo[k + 1]) * p.a.C + 3) & ~3);
-    const size_t lds = sizeof(float) * ((size_t)fmax + (LV_STAGED_DEFAULT ? (size_t)kWavesPerBlock * stage_floats(LT, p.a.C) : 0));
+    p.a.fpitch = fmax;  // trig tables follow the spectrum slice (LT >= kTrigLdsMinL)
+    const size_t trig = LT >= kTrigLdsMinL && !LV_STAGED_DEFAULT
+                            ? (size_t)kWavesPerBlock * p.a.Sw * TrigLds<LT>::kRow : 0;
+    const size_t lds = sizeof(float) * ((size_t)fmax + trig + (LV_STAGED_DEFAULT ? (size_t)kWavesPerBlock * stage_floats(LT, p.a.C) : 0));
     const dim3 grid(p.gx, p.gy), block(kThreads);
     if (p.fused) {  // the fused path takes a shared spectrum (ActionNet's item_rep)
       if (bf16)

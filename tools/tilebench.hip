@@ -73,6 +73,41 @@ static double run_tile(ActionArgs a, int nseg, int reps, float* out, std::vector
   return ms * 1e3 / reps;
 }
 
+// pipelined tile kernel: nseg waves per block, grid G blocks (0 = one block per group)
+static double run_tilep(ActionArgs a, int nseg, int G, int wt, int reps, float* out,
+                        std::vector<float>& ref, int64_t n, bool check) {
+  plan(nseg, 40.0, a.seg_lo);
+  int fp = 0;
+  for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
+  a.fpitch = (fp + 3) & ~3;
+  a.write_through = wt;
+  const size_t lds = 2 * (size_t)tile_stage_bytes(a.Sw, a.MC, 4) +
+                     4 * (size_t)tilep_trig_floats(a.Sw, L) + 4 * (size_t)nseg * a.fpitch;
+  const int groups = (int)((n + a.Sw - 1) / a.Sw);
+  const int gx = G <= 0 ? groups : std::min(G, groups);
+  auto k = action_fwd_tilep_kernel<L, true, float>;
+  if (check) {
+    CK(hipMemset(out, 0, (size_t)n * a.MC * 4));
+    hipLaunchKernelGGL(k, dim3(gx), dim3(64 * nseg), lds, 0, a);
+    CK(hipDeviceSynchronize());
+    std::vector<float> h((size_t)n * a.MC);
+    CK(hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < h.size(); ++i) bad += memcmp(&h[i], &ref[i], 4) != 0;
+    if (bad) printf("  MISMATCH tilep nseg=%d G=%d: %zu of %zu differ\n", nseg, gx, bad, h.size());
+  }
+  for (int w = 0; w < 20; ++w) hipLaunchKernelGGL(k, dim3(gx), dim3(64 * nseg), lds, 0, a);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, 0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(gx), dim3(64 * nseg), lds, 0, a);
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3 / reps;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 4096;
   const int reps = argc > 2 ? atoi(argv[2]) : 500;
@@ -129,7 +164,50 @@ int main(int argc, char** argv) {
     printf("tile v1 nseg=4 sc1: %.2f us\n", run_tile<16, 1>(a, 4, reps, out, dummy, n, false));
     return 0;
   }
+  if (only == 2) {  // pipelined tile kernel sweep vs the library's tile kernel (5 seg, sc1)
+    printf("n=%lld tile nseg=5 sc1: %.2f us\n", (long long)n,
+           run_tile<16, 1>(a, 5, reps, out, ref, n, true));
+    const int groups = (int)((n + a.Sw - 1) / a.Sw);
+    for (int nseg : {4, 6, 8})
+      for (int G : {256, 512, 1024, 0}) {
+        if (G > groups) continue;
+        const double t1 = run_tilep(a, nseg, G, 1, reps, out, ref, n, true);
+        const double t0 = run_tilep(a, nseg, G, 0, reps, out, ref, n, false);
+        printf("n=%lld tilep nseg=%d G=%d: sc1 %.2f  nt %.2f us  (best %.0f GB/s)\n", (long long)n,
+               nseg, G ? G : groups, t1, t0, bytes / std::min(t0, t1) / 1e3);
+      }
+    return 0;
+  }
 #ifdef LV_STAMPS
+  if (only == 3) {  // tilep phase stamps (first group of each block)
+    for (int nseg : {4, 8})
+      for (int G : {256, 683}) {
+        const int waves = G * nseg;
+        unsigned long long* sb;
+        CK(hipMalloc(&sb, (size_t)waves * 64));
+        CK(hipMemset(sb, 0, (size_t)waves * 64));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(lv_stamp_buf), &sb, sizeof(sb)));
+        const double us = run_tilep(a, nseg, G, 1, 50, out, ref, n, false);
+        std::vector<unsigned long long> hs((size_t)waves * 8);
+        CK(hipMemcpy(hs.data(), sb, hs.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, tend = 0;
+        for (int w = 0; w < waves; ++w) { t0 = std::min(t0, hs[w * 8]); tend = std::max(tend, hs[w * 8 + 6]); }
+        printf("tilep nseg=%d G=%d: %.2f us/launch, stamped span %.2f us\n", nseg, G, us, (tend - t0) * 0.01);
+        const char* names[7] = {"start", "F stage", "prologue", "chain0", "barrier0", "flush0", "rest"};
+        const int from[7] = {-1, 0, 1, 2, 3, 4, 5}, to[7] = {0, 1, 2, 3, 4, 5, 6};
+        for (int ph = 0; ph < 7; ++ph) {
+          std::vector<double> v;
+          for (int w = 0; w < waves; ++w) {
+            auto* p = &hs[w * 8];
+            v.push_back(from[ph] < 0 ? (p[0] - t0) * 0.01 : ((double)p[to[ph]] - (double)p[from[ph]]) * 0.01);
+          }
+          std::sort(v.begin(), v.end());
+          printf("  %-9s min %6.2f p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us\n", names[ph], v[0], v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+        }
+        CK(hipFree(sb));
+      }
+    return 0;
+  }
   for (int ver : {1, 2})
   for (int nseg : {4, 5, 6}) {
     const int waves = (int)((n + a.Sw - 1) / a.Sw) * nseg;
