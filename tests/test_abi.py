@@ -90,3 +90,25 @@ def test_j_table_matches_header_and_oracle():
         np.testing.assert_array_equal(lie_ref.j_table(l).numpy(), j.astype(np.float32))
     hdr = open(os.path.join(REPO, "lie-vae_amd", "csrc", "j_tables.h")).read()
     assert "#define LV_J_LMAX 20" in hdr
+
+
+def test_toy_dataset_host_side(tmp_path):
+    """ToyDataset (datasets.py:129-162): seeded spectrum of norm 10, the generator refuses
+    CPU tensors (the action runs only on the HIP path), and save/load round-trips through
+    a weights_only torch.load."""
+    from lie_vae.experiments.datasets import ToyDataset, toy_harmonics
+    h = toy_harmonics(6, 10)
+    assert h.shape == (49, 10)
+    assert torch.allclose(h.norm(), torch.tensor(10.0))
+    assert torch.equal(h, toy_harmonics(6, 10))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ToyDataset.generate(n=8, degrees=6, device="cpu")
+    q = torch.randn(5, 4)
+    x = torch.randn(5, 49, 10)
+    ds = ToyDataset(tensors=(q, h.expand(5, -1, -1), x))
+    p = str(tmp_path / "toy.pt")
+    ds.save(p)
+    back = ToyDataset(path=p)
+    assert len(back) == 5
+    for a, b in zip(ds.tensors, back.tensors):
+        assert torch.equal(a, b)
