@@ -105,6 +105,14 @@ constexpr double kTileSegCostSmall = 450.0;   // per-wave chain cost target, few
 constexpr double kTileSegCostLarge = 560.0;   // ... many groups (>= kTileManyGroups)
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
+// Paired-column tile kernel (C = 10, l <= kPairMaxL): 12 samples per block; its tile is
+// twice as large, so up to 80 KB of LDS (still 2 blocks per CU).  OFF by default: it is
+// bit-identical to the scalar tile kernel but measured slower on MI355X (B = 4,096:
+// 7.94 vs 7.38 us; 65,536: 79.7 vs 74.6 us, best segment count each) -- halving the VALU
+// stream does not pay, the kernel is bound by latency and the store path, not VALU issue
+// (DESIGN.md section 9).  LV_TILE_PAIR=1 enables it, LV_PAIR_NSEG=k sets its segment count.
+constexpr size_t kTilePairMaxLds = 80 * 1024;
+constexpr int kPairSegDefault = 7;
 
 // LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy (A/B
 // testing and diagnosis only; read once per process).
@@ -113,25 +121,34 @@ int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 
-bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
+bool plan_tile(FwdLaunch& p, int L, int out_bytes, bool pair) {
   static const int kEnvTile = env_int("LV_TILE", 1);
   static const int kEnvWT = env_int("LV_TILE_WT", -1);
+  static const int kEnvPairSeg = env_int("LV_PAIR_NSEG", 0);
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
+  a.Sw = pair ? kPairSw : 64 / a.C;
   const int64_t groups = (a.n + a.Sw - 1) / a.Sw;
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
   const double target = groups < kTileManyGroups ? kTileSegCostSmall : kTileSegCostLarge;
-  const int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
+  int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
+  if (pair) nseg = std::min(L + 1, kEnvPairSeg > 0 ? std::min(8, kEnvPairSeg) : kPairSegDefault);
   plan_segments(L, nseg, kPrologueFused, false, a.seg_lo);
   int fp = 0;
   for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
   a.fpitch = (fp + 3) & ~3;
-  const size_t lds = (size_t)tile_stage_bytes(a.Sw, a.MC, out_bytes) + sizeof(float) * nseg * a.fpitch;
-  if (lds > kTileMaxLds || groups > 0x7fffffff) return false;
+  const size_t trig = pair ? (size_t)a.Sw * (6 * ((L + 1 + 3) & ~3) + 4) : 0;  // TrigLds<L>::kRow
+  const size_t lds = (size_t)tile_stage_bytes(a.Sw, a.MC, out_bytes) +
+                     sizeof(float) * ((size_t)nseg * a.fpitch + trig);
+  if (lds > (pair ? kTilePairMaxLds : kTileMaxLds) || groups > 0x7fffffff) {
+    a.Sw = 64 / a.C;
+    return false;
+  }
   a.write_through = (int64_t)a.n * a.MC * out_bytes <= kWriteThroughMaxBytes ? 1 : 0;
   if (kEnvWT >= 0) a.write_through = kEnvWT;
   p.tile = true;
+  p.pair = pair;
   p.lds = lds;
   p.gx = (int)groups;
   p.gy = nseg;
@@ -185,7 +202,11 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   p.fused = fused;
   p.dtype = out_dtype;
   p.stream = stream;
-  if (Fstride == 0 && plan_tile(p, L, out_dtype == LV_DTYPE_BF16 ? 2 : 4))
+  static const int kEnvPair = env_int("LV_TILE_PAIR", 0);
+  const int ob = out_dtype == LV_DTYPE_BF16 ? 2 : 4;
+  if (Fstride == 0 && kEnvPair && C == kPairC && L <= kPairMaxL && plan_tile(p, L, ob, true))
+    return dispatch_L<FwdLauncher>(L, p);
+  if (Fstride == 0 && plan_tile(p, L, ob, false))
     return dispatch_L<FwdLauncher>(L, p);
   const double P = fused ? kPrologueFused : kPrologueFwd;
   const int nseg = choose_nseg(n, p.a.Sw, L, P, false);

@@ -478,6 +478,164 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   LV_STAMP(4);
 }
 
+// ------------------------------------------------------- paired tile forward (C = 10)
+// The tile kernel with each lane owning TWO adjacent columns (c, c+1) of one sample:
+// every chain operand is a column pair, so the X rotations and the J products run as
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32, two columns per VALU slot; the cos/sin
+// multiples and J's literal coefficients are broadcast via op_sel).  A wave then holds
+// Sw = 12 samples x 5 column pairs, so the per-sample prologue is also amortised over
+// twice the samples.  Same rounding sequence per element as the scalar chain.
+// C is a compile-time 10 (ActionNet's default rep_copies, the BASELINE configs): spectrum
+// reads and LDS tile writes use immediate offsets.
+typedef float lv_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ lv_f2 splat2(float v) { return (lv_f2){v, v}; }
+
+template <int l, int A, int LT>
+__device__ __forceinline__ void xrot2(const TrigTab<LT>& t, const lv_f2 (&x)[2 * l + 1],
+                                      lv_f2 (&y)[2 * l + 1]) {
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) {
+      y[i] = x[i];
+    } else if constexpr (f > 0) {
+      y[i] = __builtin_elementwise_fma(splat2(t.c[A][f]), x[i], splat2(t.s[A][f]) * x[2 * l - i]);
+    } else {
+      y[i] = __builtin_elementwise_fma(splat2(t.c[A][-f]), x[i],
+                                       -(splat2(t.s[A][-f]) * x[2 * l - i]));
+    }
+  });
+}
+
+// xrot2 with the multiples read from a per-sample LDS row (TrigLds layout).
+template <int l, int A, int LT>
+__device__ __forceinline__ void xrot2_lds(const float* tj, const lv_f2 (&x)[2 * l + 1],
+                                          lv_f2 (&y)[2 * l + 1]) {
+  constexpr int TP = TrigLds<LT>::TP;
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) {
+      y[i] = x[i];
+    } else if constexpr (f > 0) {
+      y[i] = __builtin_elementwise_fma(splat2(tj[2 * A * TP + f]), x[i],
+                                       splat2(tj[(2 * A + 1) * TP + f]) * x[2 * l - i]);
+    } else {
+      y[i] = __builtin_elementwise_fma(splat2(tj[2 * A * TP - f]), x[i],
+                                       -(splat2(tj[(2 * A + 1) * TP - f]) * x[2 * l - i]));
+    }
+  });
+}
+
+template <int l>
+__device__ __forceinline__ void jmul2(const lv_f2 (&x)[2 * l + 1], lv_f2 (&y)[2 * l + 1]) {
+  constexpr int n = 2 * l + 1;
+  constexpr const float* J = lv_j::jtab<l>();
+  sfor<n>([&](auto P) {
+    constexpr int p = LV_CV(P);
+    lv_f2 acc = splat2(0.f);
+    sfor<n>([&](auto K) {
+      constexpr int k = LV_CV(K);
+      constexpr float v = J[p * n + k];
+      if constexpr (v != 0.f) acc = __builtin_elementwise_fma(splat2(v), x[k], acc);
+    });
+    y[p] = acc;
+  });
+}
+
+constexpr int kPairC = 10;
+constexpr int kPairSw = 64 / (kPairC / 2);  // 12 samples per wave
+constexpr int kPairMaxL = 12;
+
+template <int LT, bool FUSED, typename OutT>
+__global__ __launch_bounds__(512) void action_fwd_tile_pair_kernel(ActionArgs a) {
+  constexpr int C = kPairC, CP = C / 2, Sw = kPairSw;
+  constexpr int64_t MC = (int64_t)(LT + 1) * (LT + 1) * C;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane / CP;  // 12 for the 4 spare lanes
+  const int cp = lane - j * CP;
+  const int lo = a.seg_lo[wave], hi = a.seg_lo[wave + 1];
+  const int rows_lo = lo * lo;
+  const int frows = fseg_rows(lo, hi);
+  const int64_t s0 = (int64_t)blockIdx.x * Sw;
+  const int Sv = (int)min((int64_t)Sw, a.n - s0);  // >= 1: grid = ceil(n / Sw)
+  const bool active = j < Sv;
+  const int64_t s = active ? s0 + j : s0;  // idle lanes mirror a valid sample
+  LaneIn in;
+  lane_load<FUSED>(a, s, in);
+  constexpr int kFPer = 6;
+  float fv[kFPer];
+  const int fcnt = (hi * hi - rows_lo) * C;
+  const float* fsrc = a.F + rows_lo * C;
+#pragma unroll
+  for (int k = 0; k < kFPer; ++k) {
+    const int e = lane + 64 * k;
+    fv[k] = e < fcnt ? fsrc[e] : 0.f;
+  }
+  // (cos, sin) multiples: one LDS row per sample, shared by the block's waves.  Every
+  // wave fills all rows (lanes cp < 3 one angle each) with identical values, so each wave
+  // only needs its own writes to have landed -- no block barrier (the chain would wait
+  // for the slowest prologue) and no register table (it would cost 6(l+1) VGPRs).
+  constexpr int kRow = TrigLds<LT>::kRow;
+  const int stage_bytes = tile_stage_bytes(Sw, MC, (int)sizeof(OutT));
+  float* trow = lds + (stage_bytes >> 2) + (int)(blockDim.x >> 6) * a.fpitch;
+  {
+    float c1[3], s1[3];
+    lane_angles<FUSED>(a, in, s, active, cp, FUSED && a.ang_out && wave == 0, c1, s1);
+    if (j < Sw)
+      for (int q = cp; q < 3; q += CP) trig_row_fill<LT>(trow + j * kRow, c1, s1, q, LT);
+  }
+  const float* tj = trow + min(j, Sw - 1) * kRow;
+  // wave-private spectrum slice as [column pair][row][2]
+  float* Fw = lds + (stage_bytes >> 2) + wave * a.fpitch;
+#pragma unroll
+  for (int k = 0; k < kFPer; ++k) {
+    const int e = lane + 64 * k;
+    if (e < fcnt) {
+      const int r = e / C, cc = e - r * C;
+      Fw[((cc >> 1) * frows + r) * 2 + (cc & 1)] = fv[k];
+    }
+  }
+  for (int e = lane + 64 * kFPer; e < fcnt; e += 64) {
+    const int r = e / C, cc = e - r * C;
+    Fw[((cc >> 1) * frows + r) * 2 + (cc & 1)] = fsrc[e];
+  }
+  wave_lds_sync();
+
+  OutT* gout = reinterpret_cast<OutT*>(a.out) + s0 * MC;
+  const int mis = (int)(reinterpret_cast<uintptr_t>(gout) & 15);
+  char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
+  OutT* st_lane = reinterpret_cast<OutT*>(stage_b) + j * MC + 2 * cp;
+  const lv_f2* Fl = reinterpret_cast<const lv_f2*>(Fw + cp * frows * 2) - rows_lo;
+
+  sfor<LT + 1>([&](auto Lc) {
+    constexpr int l = LV_CV(Lc);
+    if (l >= lo && l < hi) {
+      constexpr int nn = 2 * l + 1;
+      constexpr int r0 = l * l;
+      lv_f2 x[nn], y[nn];
+      sfor<nn>([&](auto K) { x[LV_CV(K)] = Fl[r0 + LV_CV(K)]; });
+      xrot2_lds<l, 2, LT>(tj, x, y);
+      jmul2<l>(y, x);
+      xrot2_lds<l, 1, LT>(tj, x, y);
+      jmul2<l>(y, x);
+      xrot2_lds<l, 0, LT>(tj, x, y);
+      if (active) {
+        OutT* d = st_lane + r0 * C;
+        sfor<nn>([&](auto I) {
+          constexpr int i = LV_CV(I);
+          d[i * C] = tile_cvt(y[i].x, (OutT*)nullptr);
+          d[i * C + 1] = tile_cvt(y[i].y, (OutT*)nullptr);
+        });
+      }
+    }
+  });
+  __syncthreads();
+  tile_flush_rt<OutT>(gout, stage_b, mis, Sv * (int)MC * (int)sizeof(OutT), a.write_through);
+}
+
 // ------------------------------------------------------------ Wigner-D blocks
 // Column q of D_l = chain applied to e_q; one thread per (sample, q), one kernel per
 // degree.  D is (n, dsz) with block l row-major at offset off.
@@ -510,6 +668,7 @@ struct FwdLaunch {
   int gx, gy;
   bool fused;
   bool tile;     // tile kernel (shared spectrum; gy = waves per block)
+  bool pair;     // ... its paired-column variant (C = 10, l <= kPairMaxL)
   size_t lds;    // tile kernel dynamic LDS bytes
   int dtype;
   hipStream_t stream;
@@ -520,6 +679,23 @@ struct FwdLauncher {
   using Args = FwdLaunch;
   static int run(FwdLaunch& p) {
     const bool bf16 = p.dtype == LV_DTYPE_BF16;
+    if constexpr (LT <= kPairMaxL) {
+      if (p.tile && p.pair) {
+        const dim3 grid(p.gx), block(64 * p.gy);
+        if (p.fused) {
+          if (bf16)
+            hipLaunchKernelGGL((action_fwd_tile_pair_kernel<LT, true, __hip_bfloat16>), grid, block, p.lds, p.stream, p.a);
+          else
+            hipLaunchKernelGGL((action_fwd_tile_pair_kernel<LT, true, float>), grid, block, p.lds, p.stream, p.a);
+        } else {
+          if (bf16)
+            hipLaunchKernelGGL((action_fwd_tile_pair_kernel<LT, false, __hip_bfloat16>), grid, block, p.lds, p.stream, p.a);
+          else
+            hipLaunchKernelGGL((action_fwd_tile_pair_kernel<LT, false, float>), grid, block, p.lds, p.stream, p.a);
+        }
+        LV_RETURN_LAUNCH("action_fwd_tile_pair_kernel");
+      }
+    }
     if (p.tile) {
       const dim3 grid(p.gx), block(64 * p.gy);
       if (p.fused) {

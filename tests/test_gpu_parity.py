@@ -364,3 +364,42 @@ def test_toy_dataset_generate(gpu_device):
     # norm preserved per sample and column: D is orthogonal
     np.testing.assert_allclose(np.linalg.norm(x, axis=1), np.linalg.norm(h, axis=1),
                                rtol=1e-5)
+
+
+_PAIR_CHECK = r"""
+import sys, torch
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import lie_vae._ops as ops
+import lie_vae.lie_tools as lt
+dev = torch.device("cuda:0")
+for L, n, transpose, bf16 in [(10, 4099, False, False), (10, 4096, True, False),
+                              (3, 1000, False, False), (12, 777, False, True)]:
+    gen = torch.Generator().manual_seed(7 + L + n)
+    v = torch.randn(n, 3, generator=gen).to(dev)
+    F11 = torch.randn((L + 1) ** 2, 11, generator=gen).to(dev)
+    F10 = F11[:, :10].contiguous()
+    od = torch.bfloat16 if bf16 else torch.float32
+    a = ops.fused_exp_action(None, v, F10, L, transpose=transpose, out_dtype=od)
+    b = ops.fused_exp_action(None, v, F11, L, transpose=transpose, out_dtype=od)
+    assert torch.equal(a, b[..., :10]), ("fused", L, n, transpose, bf16)
+    ang = lt.group_matrix_to_eazyz(lt.rodrigues(v))
+    a = ops.group_action(ang, F10, L, transpose=transpose, out_dtype=od)
+    b = ops.group_action(ang, F11, L, transpose=transpose, out_dtype=od)
+    assert torch.equal(a, b[..., :10]), ("angles", L, n, transpose, bf16)
+print("paired == scalar: ok")
+"""
+
+
+def test_paired_column_kernel_bitwise():
+    """The opt-in paired-column (packed fp32) tile kernel (LV_TILE_PAIR=1, C = 10) against
+    the scalar tile kernel (C = 11): columns are independent and both chains round
+    identically, so the first 10 columns must agree bit for bit (fused and angle inputs,
+    ragged last group, transpose, bf16 output).  The library reads the switch once per
+    process, hence the child process."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, LV_TILE_PAIR="1")
+    r = subprocess.run([sys.executable, "-c", _PAIR_CHECK, os.path.join(REPO, "lie-vae_amd"), REPO],
+                       env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
