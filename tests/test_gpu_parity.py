@@ -403,3 +403,61 @@ def test_paired_column_kernel_bitwise():
     r = subprocess.run([sys.executable, "-c", _PAIR_CHECK, os.path.join(REPO, "lie-vae_amd"), REPO],
                        env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+# ------------------------------------------------ end to end: VAE glue + IWAE (a11-a16, f3)
+def _vae_oracle(vae, x, eps, L, k=10):
+    """The toy-mode VAE pipeline restated with oracle functions on the CPU (vae.py:113-204,
+    reparameterize.py:100-278, decoders.py:47-56): returns x_recon (n,B,M,C), the
+    summed-squares recon loss (n,B), log q(z|x) (n,B) and kl (B,)."""
+    from oracle import lie_ref
+    rep = vae.rep_group
+    with torch.no_grad():
+        h = vae.encoder(x)
+        mu = lie_ref.so3_exp(rep.mean_module.map(h))
+        sig = lie_ref.n0_sigma(rep.reparameterize.sigma_linear(h))
+        v = lie_ref.n0_sample(sig, eps)
+        z = lie_ref.so3_sample(mu, v)
+        n, B = eps.shape[:2]
+        ang = lie_ref.mat_to_eazyz(z.reshape(-1, 3, 3))
+        xr = lie_ref.action_decode(ang, vae.decoder.item_rep, L).reshape(n, B, *x.shape[1:])
+        recon = ((xr - x) ** 2).sum(-1).sum(-1)
+        lq = lie_ref.so3_log_posterior(v, sig, k)
+        kl = (lq + math.log(8 * math.pi ** 2)).mean(0)
+    return xr, recon, lq, kl
+
+
+def test_vae_toy_elbo_and_log_likelihood_vs_oracle(gpu_device):
+    """Toy-mode VAE (MLP encoder, SO(3) latent with AlgebraMean, ActionNet l = 6, C = 10,
+    no deconv): ELBO terms with injected eps, and the importance-weighted log-likelihood
+    (vae.py:164-171) with the device RNG replayed, against the oracle pipeline."""
+    from lie_vae.experiments.vae import VAE
+    L, B, n = 6, 16, 5
+    torch.manual_seed(3)
+    vae = VAE(latent_mode='so3', decoder_mode='action', degrees=L, encode_mode='toy',
+              deconv_mode='toy', rep_copies=10, mean_mode='alg')
+    x = torch.randn(B, (L + 1) ** 2, 10)
+    eps = torch.randn(n, B, 3)
+    xr_ref, recon_ref, lq_ref, kl_ref = _vae_oracle(vae, x, eps, L)
+    vg = VAE(latent_mode='so3', decoder_mode='action', degrees=L, encode_mode='toy',
+             deconv_mode='toy', rep_copies=10, mean_mode='alg')
+    vg.load_state_dict(vae.state_dict())
+    vg = vg.to(gpu_device)
+    xg = x.to(gpu_device)
+    with torch.no_grad():
+        recon, kl_sum, _ = vg.elbo(xg, n, eps=eps.to(gpu_device))
+        xr = vg.forward(xg, n, eps=eps.to(gpu_device))
+    assert_normwise(host(xr).reshape(n * B, -1), xr_ref.numpy().reshape(n * B, -1), 1e-5,
+                    what="x_recon")
+    np.testing.assert_allclose(host(recon), recon_ref.numpy(), rtol=1e-4)
+    np.testing.assert_allclose(host(kl_sum), kl_ref.numpy(), rtol=1e-4, atol=1e-4)
+    # IWAE: log_likelihood draws eps with torch.randn on the device; replay the same draw
+    torch.cuda.manual_seed(11)
+    eps2 = torch.randn((n, B, 3), device=gpu_device)
+    torch.cuda.manual_seed(11)
+    with torch.no_grad():
+        ll = vg.log_likelihood(xg, n)
+    _, recon2, lq2, _ = _vae_oracle(vae, x, eps2.cpu(), L)
+    w = -recon2 - math.log(8 * math.pi ** 2) - lq2
+    ll_ref = (torch.logsumexp(w, 0) - math.log(n)).mean()
+    np.testing.assert_allclose(float(ll), float(ll_ref), rtol=1e-4)
