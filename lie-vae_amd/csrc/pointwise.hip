@@ -337,6 +337,105 @@ __global__ void so3_logpost_bwd_k(const float* v, const float* sigma, const floa
   }
 }
 
+// Wave-per-element variants: lane t holds wrapped term t - k (2k+1 <= 64), max and sum
+// over the terms by cross-lane reductions.  The thread-per-element kernels above run the
+// 2k+1 terms (x2 passes, x3 in backward) serially per thread: at training sizes
+// (ns * B = 512) that is a latency chain of ~60 transcendental terms on a few waves.
+// Same per-term arithmetic; only the order of the exp-sum (and gradient sums) differs.
+constexpr int kWaveMaxK = 31;
+constexpr int64_t kWaveMaxElems = 1 << 16;  // beyond: enough elements to fill the chip per thread
+
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+#define LV_FOR_EACH_WAVE(i, n)                                                          \
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < (n);        \
+       i += ((int64_t)gridDim.x * blockDim.x) >> 6)
+
+__global__ void so3_logpost_fwd_wave_k(const float* v, const float* sigma, float* out, int64_t ns,
+                                       int64_t B, int k) {
+  const int lane = threadIdx.x & 63;
+  const bool on = lane < 2 * k + 1;
+  LV_FOR_EACH_WAVE(i, ns * B) {
+    const int64_t b = i % B;
+    float a[3], sg[3], var[3], ls[3];
+    ld(v + i * 3, a);
+    ld(sigma + b * 3, sg);
+    for (int j = 0; j < 3; ++j) { var[j] = sg[j] * sg[j]; ls[j] = logf(sg[j]); }
+    const float th = norm3(a);
+    const float u[3] = {a[0] / th, a[1] / th, a[2] / th};
+    const float term = on ? logpost_term(lane - k, th, u, var, ls) : -INFINITY;
+    const float m = wave_max(term);
+    const float sum = wave_sum(on ? expf(term - m) : 0.f);
+    if (lane == 0) out[i] = m + logf(sum);
+  }
+}
+
+__global__ void so3_logpost_bwd_wave_k(const float* v, const float* sigma, const float* gout,
+                                       float* gv, float* gsig, int64_t ns, int64_t B, int k) {
+  const int lane = threadIdx.x & 63;
+  const bool on = lane < 2 * k + 1;
+  const int t = lane - k;
+  LV_FOR_EACH_WAVE(b, B) {
+    float sg[3], var[3], ls[3];
+    ld(sigma + b * 3, sg);
+    for (int j = 0; j < 3; ++j) { var[j] = sg[j] * sg[j]; ls[j] = logf(sg[j]); }
+    float gsacc[3] = {0.f, 0.f, 0.f};
+    for (int64_t s = 0; s < ns; ++s) {
+      const int64_t i = s * B + b;
+      float a[3];
+      ld(v + i * 3, a);
+      const float th = norm3(a);
+      const float u[3] = {a[0] / th, a[1] / th, a[2] / th};
+      const float term = on ? logpost_term(t, th, u, var, ls) : -INFINITY;
+      const float m = wave_max(term);
+      const float lse = m + logf(wave_sum(on ? expf(term - m) : 0.f));
+      float gth = 0.f, gu[3] = {0.f, 0.f, 0.f};
+      if (on) {
+        const float w = gout[i] * expf(term - lse);
+        const float thk = th + (float)t * kTwoPi;
+        float dth = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const float x = u[j] * thk;
+          dth -= x * u[j] / var[j];
+          gu[j] = -(w * x * thk / var[j]);
+          gsacc[j] += w * ((x * x) / (var[j] * sg[j]) - 1.f / sg[j]);
+        }
+        if (thk * thk >= 1e-3f) dth += 2.f * thk / (thk * thk);
+        const float den = 2.f - 2.f * cosf(thk);
+        if (den >= 1e-3f) dth -= 2.f * sinf(thk) / den;
+        gth = w * dth;
+      }
+      gth = wave_sum(gth);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) gu[j] = wave_sum(gu[j]);
+      if (lane == 0) {
+        float o[3];
+        polar_vjp(a, th, gu, gth, o);
+        st(gv + i * 3, o);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gsacc[j] = wave_sum(gsacc[j]);
+    if (lane == 0) st(gsig + b * 3, gsacc);
+  }
+}
+
+inline dim3 grid_for_waves(int64_t nwaves) {
+  int64_t b = (nwaves * 64 + kBlock - 1) / kBlock;
+  if (b > 65536) b = 65536;
+  return dim3((unsigned)b);
+}
+
 }  // namespace lv
 
 using namespace lv;
@@ -460,6 +559,12 @@ int lv_so3_log_posterior_fwd(const float* v, const float* sigma, float* out, int
   LV_CHECK_ARG(ns >= 0 && B >= 0, "bad sizes");
   LV_CHECK_ARG(k >= 0 && k <= kMaxWrap, "k must be in [0, %d]", kMaxWrap);
   LV_PTRS(v && sigma && out);
+  if (n > 0 && k <= kWaveMaxK && n <= kWaveMaxElems) {
+    clear_error();
+    hipLaunchKernelGGL(so3_logpost_fwd_wave_k, grid_for_waves(n), dim3(kBlock), 0,
+                       (hipStream_t)stream, v, sigma, out, ns, B, k);
+    LV_RETURN_LAUNCH("so3_logpost_fwd_wave_k");
+  }
   LV_LAUNCH1(so3_logpost_fwd_k, n, v, sigma, out, ns, B, k);
 }
 int lv_so3_log_posterior_bwd(const float* v, const float* sigma, const float* gout, float* gv,
@@ -471,6 +576,12 @@ int lv_so3_log_posterior_bwd(const float* v, const float* sigma, const float* go
   if (ns == 0) {
     (void)hipMemsetAsync(gsigma, 0, sizeof(float) * 3 * B, (hipStream_t)stream);
     return LV_OK;
+  }
+  if (n > 0 && k <= kWaveMaxK && n <= kWaveMaxElems) {
+    clear_error();
+    hipLaunchKernelGGL(so3_logpost_bwd_wave_k, grid_for_waves(n), dim3(kBlock), 0,
+                       (hipStream_t)stream, v, sigma, gout, gv, gsigma, ns, B, k);
+    LV_RETURN_LAUNCH("so3_logpost_bwd_wave_k");
   }
   LV_LAUNCH1(so3_logpost_bwd_k, n, v, sigma, gout, gv, gsigma, ns, B, k);
 }
