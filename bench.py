@@ -3,15 +3,22 @@
 
 One step = one pass of the fused hot path (z = exp(v) -> ZYZ Euler -> block-diagonal
 real Wigner-D(z) · F, l_max = 10, C = 10, fp32) over one batch of 4096 synthetic
-samples already resident in HBM.  With --gpus N (one process per GPU, launched by
-torch.distributed.run) every rank runs its own 4096-sample batches: the path
-partitions by sample with no data-path collective, so scaling is weak and the
-value is the sum over ranks (all-rank samples / max-over-ranks time).
+samples already resident in HBM.  ``--gpus N`` runs one process per GPU: started
+without a torch.distributed environment the script hands itself to
+``torch.distributed.run`` before any HIP call (lie_vae/experiments/launch.py); started
+by the driver's own ``torch.distributed.run`` it is that rank.  Every rank runs its
+own 4096-sample batches: the path partitions by sample with no data-path collective,
+so scaling is weak and the value is all ranks' samples / max-over-ranks time.  The
+N = 1 output is unchanged by the launcher (no process group, no hand-off).
 
-Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §Bench):
+Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §6):
   value            samples/s, whole job
-  roofline         HBM roofline of the fused kernel from live HIP-event timing
-  cpu_baseline     the CPU oracle (reference op sequence, torch CPU) on a bounded sample
+  roofline         HBM roofline of the fused kernel from live HIP-event timing (hot
+                   Infinity Cache: back-to-back launches); ``cache_cold`` repeats it
+                   with a 512 MiB scrub write between launches (> the 256 MiB MALL)
+  cpu_baseline     the CPU oracle (reference op sequence, torch CPU) on a bounded
+                   sample: all usable cores + 1 thread, forward and forward+backward
+  fwd_bwd          the training direction on the GPU (fused forward + backward kernels)
 """
 import argparse
 import ctypes
@@ -26,7 +33,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lie-vae_amd"))
 sys.path.insert(0, REPO)
 
+from lie_vae.experiments import launch  # noqa: E402  (imports torch only; no HIP call)
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+SCRUB_BYTES = 512 << 20  # > 256 MiB Infinity Cache (MI355X_MICROARCH.md:40)
 
 
 def parse():
@@ -41,13 +51,18 @@ def parse():
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
                     help="graph: steps captured in a hipGraph and replayed; eager: C launch loop")
     ap.add_argument("--graph-chunk", type=int, default=100)
-    ap.add_argument("--streams", type=int, default=1,
-                    help="independent batches in flight on this many HIP streams (graph mode)")
     ap.add_argument("--multistream", type=int, default=4,
                     help="also time this many independent batches in flight (extra field)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cold-launches", type=int, default=40,
+                    help="launches timed with a 512 MiB scrub between them (0: skip)")
+    ap.add_argument("--cold-only", action="store_true",
+                    help="only the scrubbed launches (for rocprofv3 kernel-trace runs)")
+    ap.add_argument("--no-fwd-bwd", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sweep", action="store_true", help="also print a batch sweep (stderr)")
+    ap.add_argument("--sweep", action="store_true", help="also report a batch sweep")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rehearse the rank plumbing on CPU (gloo, no HIP call)")
     return ap.parse_args()
 
 
@@ -57,42 +72,99 @@ def algorithmic_bytes(batch, L, C, out_bytes):
     return batch * (12 + M * C * out_bytes) + M * C * 4
 
 
+def algorithmic_bytes_bwd(batch, L, C):
+    """Backward of the fused path: read angles (12 B) + the output gradient (M·C·4) and
+    write the angle gradient (12 B) per sample; read F and write dF once."""
+    M = (L + 1) ** 2
+    return batch * (12 + M * C * 4 + 12) + 2 * M * C * 4
+
+
+def cpu_threads():
+    """Cores this process may use: its affinity set, capped by the box's CPU share
+    (OMP_NUM_THREADS, set to the allotted share on the GPU box)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        usable = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(usable, share) if share > 0 else usable), usable
+
+
 def cpu_baseline(L, C, batch, seconds):
-    """Reference op sequence on the host (oracle/lie_ref.py), timed on a bounded sample."""
+    """Reference op sequence on the host (oracle/lie_ref.py, a restatement of
+    lie_tools.py:56-64,112-180,211-253), timed on a bounded sample: forward at all usable
+    cores and at 1 thread, forward+backward at all usable cores."""
     from oracle import lie_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    threads, usable = cpu_threads()
     g = torch.Generator().manual_seed(0)
     v = torch.randn(batch, 3, generator=g)
     F = torch.randn((L + 1) ** 2, C, generator=g)
-    with torch.no_grad():
-        def run():
-            ang = lie_ref.mat_to_eazyz(lie_ref.so3_exp(v))
-            return lie_ref.block_wigner_apply(ang, F.expand(batch, -1, -1), L)
-        run()
+
+    def fwd(vv, FF):
+        ang = lie_ref.mat_to_eazyz(lie_ref.so3_exp(vv))
+        return lie_ref.block_wigner_apply(ang, FF.expand(vv.shape[0], -1, -1), L)
+
+    def timed(fn, budget, nb):
+        fn()
         n, t0 = 0, time.perf_counter()
         while True:
-            run()
+            fn()
             n += 1
             el = time.perf_counter() - t0
-            if el >= seconds:
-                break
-    return {"value": n * batch / el, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} batches x {batch} samples (exp+eazyz+action, l={L}, C={C}, fp32) "
-                      f"in {el:.1f}s, torch CPU, {threads} threads"}
+            if el >= budget:
+                return n * nb / el, n, el
+
+    torch.set_num_threads(threads)
+    with torch.no_grad():
+        fw, nf, ef = timed(lambda: fwd(v, F), seconds, batch)
+    vb = v[:1024]
+
+    def fb():
+        vg = vb.clone().requires_grad_(True)
+        Fg = F.clone().requires_grad_(True)
+        fwd(vg, Fg).square().sum().backward()
+
+    fbw, nfb, efb = timed(fb, seconds, vb.shape[0])
+    torch.set_num_threads(1)
+    with torch.no_grad():
+        f1, n1, e1 = timed(lambda: fwd(v[:1024], F), seconds / 2, 1024)
+    torch.set_num_threads(threads)
+    return {"value": fw, "unit": "samples/s", "cores": threads, "kind": "port",
+            "host_cores": os.cpu_count(), "usable_cores": usable,
+            "value_1thread": f1, "fwd_bwd_value": fbw,
+            "sample": f"forward: {nf} batches x {batch} samples (exp+eazyz+action, l={L}, "
+                      f"C={C}, fp32) in {ef:.1f}s on {threads} threads; 1 thread: {n1} x 1024 "
+                      f"in {e1:.1f}s; forward+backward: {nfb} x 1024 in {efb:.1f}s on "
+                      f"{threads} threads; torch CPU, oracle/lie_ref.py"}
+
+
+def dry_run(args, env):
+    """Rank plumbing rehearsal on CPU: gloo group, barrier-bracketed timing, max over
+    ranks, one JSON line from rank 0 -- the same control flow as the GPU run."""
+    import torch.distributed as dist
+    launch.init_process_group(env, "gloo")
+    t0 = time.perf_counter()
+    x = torch.ones(1)
+    if env.distributed:
+        dist.barrier()
+        dist.all_reduce(x)
+        dist.barrier()
+    wall = launch.max_over_ranks(time.perf_counter() - t0)
+    if env.rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": env.world, "ranks_seen": int(x.item()),
+                          "local_rank": env.local_rank, "wall_s": wall}), flush=True)
+    if env.distributed:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    env = launch.ensure_ranks(args.gpus, os.path.abspath(__file__))
+    if args.dry_run:
+        return dry_run(args, env)
+    td = launch.init_process_group(env, "nccl")
+    rank, world = env.rank, env.world
+    dev = torch.device("cuda", env.local_rank)
     torch.cuda.set_device(dev)
 
     from lie_vae import _lib
@@ -101,106 +173,115 @@ def main():
     M = (L + 1) ** 2
     out_dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     dt = _lib.LV_DTYPE_BF16 if args.dtype == "bf16" else _lib.LV_DTYPE_F32
+    out_bytes = 2 if args.dtype == "bf16" else 4
+    abytes = algorithmic_bytes(B, L, C, out_bytes)
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     v = torch.randn(B, 3, generator=g).to(dev)
     F = torch.randn(M, C, generator=g).to(dev)
-    nstreams = max(1, args.streams if args.launch == "graph" else 1)
-    outs = [torch.empty(B, M, C, device=dev, dtype=out_dtype) for _ in range(nstreams)]
-    out = outs[0]
+    out = torch.empty(B, M, C, device=dev, dtype=out_dtype)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
-    def launch(k, s=sp, o=None):
+    def launch_k(k, s=sp, o=None, vv=None, nb=B):
         o = out if o is None else o
-        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(v), P(F), 0, P(o), dt, None, B, L, C, 0,
-                                                k, s)
+        vv = v if vv is None else vv
+        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(vv), P(F), 0, P(o), dt, None, nb, L, C,
+                                                0, k, s)
         if rc:
             raise RuntimeError(_lib.last_error())
+
+    def cold(nlaunch):
+        """Per-launch kernel time with a 512 MiB scrub write between launches, so neither
+        the output nor the inputs are resident in the 256 MiB Infinity Cache."""
+        scrub = torch.empty(SCRUB_BYTES // 4, device=dev, dtype=torch.float32)
+        evs = []
+        for i in range(nlaunch + 2):
+            scrub.fill_(float(i))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            launch_k(1)
+            e1.record(stream)
+            evs.append((e0, e1))
+        torch.cuda.synchronize(dev)
+        ts = sorted(e0.elapsed_time(e1) / 1e3 for e0, e1 in evs[2:])
+        del scrub
+        med = ts[len(ts) // 2]
+        return {"launches": nlaunch, "us_median": med * 1e6, "us_min": ts[0] * 1e6,
+                "achieved": abytes / med / 1e9, "frac": abytes / med / 1e9 / HBM_PEAK_GBS,
+                "scrub_bytes": SCRUB_BYTES}
+
+    if args.cold_only:
+        rec = cold(max(1, args.cold_launches))
+        if rank == 0:
+            print(json.dumps({"cache_cold": rec}), flush=True)
+        return
 
     graph = None
     chunk = max(1, min(args.graph_chunk, args.steps))
     if args.launch == "graph":
-        launch(1)
+        launch_k(1)
         torch.cuda.synchronize(dev)
         s = torch.cuda.Stream(dev)
         s.wait_stream(stream)
         graph = torch.cuda.CUDAGraph()
-        if nstreams > 1:
-            chunk = max(nstreams, chunk - chunk % nstreams)
-            side = [torch.cuda.Stream(dev) for _ in range(nstreams)]
         with torch.cuda.graph(graph, stream=s):
-            if nstreams == 1:
-                launch(chunk, ctypes.c_void_p(s.cuda_stream))
-            else:  # fork: independent batches on parallel graph branches, then join
-                for t in side:
-                    t.wait_stream(s)
-                for t, o in zip(side, outs):
-                    launch(chunk // nstreams, ctypes.c_void_p(t.cuda_stream), o)
-                for t in side:
-                    s.wait_stream(t)
+            launch_k(chunk, ctypes.c_void_p(s.cuda_stream))
         torch.cuda.synchronize(dev)
 
     def run_steps(k):
         if graph is None:
-            launch(k)
+            launch_k(k)
             return
         full, rem = divmod(k, chunk)
         for _ in range(full):
             graph.replay()
         if rem:
-            launch(rem)
+            launch_k(rem)
 
     run_steps(args.warmup)
     torch.cuda.synchronize(dev)
-    if dist:
+    if td:
         td.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(torch.cuda.current_stream(dev))
+    ev0.record(stream)
     run_steps(args.steps)
-    ev1.record(torch.cuda.current_stream(dev))
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if dist:
+    if td:
         td.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    el = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist:
-        td.all_reduce(el, op=td.ReduceOp.MAX)
-    wall_max = float(el.item())
+    wall_max = launch.max_over_ranks(wall, dev)
 
-    samples = B * args.steps * world
-    value = samples / wall_max
+    value = B * args.steps * world / wall_max
     per_launch_s = gpu_ms / 1e3 / args.steps
-    out_bytes = 2 if args.dtype == "bf16" else 4
-    abytes = algorithmic_bytes(B, L, C, out_bytes)
     achieved = abytes / per_launch_s / 1e9
 
-    sweep = []
+    sweep = None
     if args.sweep and rank == 0:
+        sweep = []
         for nb in (4096, 16384, 65536, 262144):
             vv = torch.randn(nb, 3, device=dev)
             oo = torch.empty(nb, M, C, device=dev, dtype=out_dtype)
-            for rep in range(2):
+            reps = 50
+            for _ in range(2):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                reps = 50
-                e0.record()
-                rc = lib.lv_fused_exp_action_fwd_repeat(None, P(vv), P(F), 0, P(oo), dt, None, nb,
-                                                        L, C, 0, reps, sp)
-                e1.record()
+                e0.record(stream)
+                launch_k(reps, o=oo, vv=vv, nb=nb)
+                e1.record(stream)
                 torch.cuda.synchronize(dev)
             t = e0.elapsed_time(e1) / 1e3 / reps
             gbs = algorithmic_bytes(nb, L, C, out_bytes) / t / 1e9
             sweep.append({"batch": nb, "us": t * 1e6, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS})
             del vv, oo
-        print(json.dumps({"sweep": sweep}), file=sys.stderr)
 
     # independent batches on parallel streams (same kernel): aggregate throughput
     multi = None
-    if args.launch == "graph" and nstreams == 1 and args.multistream > 1:
+    if args.launch == "graph" and args.multistream > 1:
         ms = args.multistream
         mouts = [torch.empty(B, M, C, device=dev, dtype=out_dtype) for _ in range(ms)]
         side = [torch.cuda.Stream(dev) for _ in range(ms)]
@@ -212,7 +293,7 @@ def main():
             for t in side:
                 t.wait_stream(s2)
             for t, o in zip(side, mouts):
-                launch(mchunk // ms, ctypes.c_void_p(t.cuda_stream), o)
+                launch_k(mchunk // ms, ctypes.c_void_p(t.cuda_stream), o)
             for t in side:
                 s2.wait_stream(t)
         reps = max(1, args.steps // mchunk)
@@ -229,10 +310,17 @@ def main():
                  "aggregate_GBs": abytes * reps * mchunk / el2 / 1e9}
         del mouts
 
+    cache_cold = cold(args.cold_launches) if args.cold_launches > 0 and rank == 0 else None
+
+    fwd_bwd = None
+    if not args.no_fwd_bwd and rank == 0 and args.dtype == "f32":
+        fwd_bwd = bench_fwd_bwd(v, F, L, dev, stream)
+
     traffic = None
     tpath = os.path.join(REPO, "profiles", f"traffic_B{B}_L{L}_C{C}_{args.dtype}.json")
     if os.path.exists(tpath):
-        traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        with open(tpath) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -256,17 +344,68 @@ def main():
                                    "(lv_fused_exp_action_fwd)",
                        "batch_per_gpu": B, "global_batch": B * world, "l_max": L,
                        "channels": C, "parallelism": f"sample-sharded x{world}, no collective",
-                       "launch": args.launch, "streams": nstreams},
+                       "launch": args.launch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": abytes,
-                         "us_per_launch_events": per_launch_s * 1e6},
+                         "us_per_launch_events": per_launch_s * 1e6,
+                         "cache": "hot (back-to-back launches)"},
+            "cache_cold": cache_cold,
             "cpu_baseline": cpu,
+            "fwd_bwd": fwd_bwd,
             "multistream": multi,
+            "sweep": sweep,
         }
         print(json.dumps(rec), flush=True)
-    if dist:
+    if td:
         td.destroy_process_group()
+
+
+def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
+    """Training direction at the metric size: the fused forward and the full backward
+    (group-action backward kernels + ZYZ and exp VJPs) through the autograd ops."""
+    import lie_vae._ops as ops
+    B, C = v.shape[0], F.shape[1]
+    vg = v.clone().requires_grad_(True)
+    Fg = F.clone().requires_grad_(True)
+    gout = torch.randn(B, (L + 1) ** 2, C, device=dev)
+
+    def step():
+        vg.grad = None
+        Fg.grad = None
+        out = ops.fused_exp_action(None, vg, Fg, L)
+        out.backward(gout)
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    # backward kernels alone (same autograd graph, forward excluded)
+    out = ops.fused_exp_action(None, vg, Fg, L)
+    torch.cuda.synchronize(dev)
+    tb = []
+    for _ in range(20):
+        out = ops.fused_exp_action(None, vg, Fg, L)
+        b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        b0.record(stream)
+        out.backward(gout)
+        b1.record(stream)
+        tb.append((b0, b1))
+    torch.cuda.synchronize(dev)
+    tbs = sorted(b0.elapsed_time(b1) / 1e3 for b0, b1 in tb)
+    tb_med = tbs[len(tbs) // 2]
+    bb = algorithmic_bytes_bwd(B, L, C)
+    return {"value": B / t, "unit": "samples/s", "us_per_step": t * 1e6,
+            "bwd_us_median": tb_med * 1e6, "bwd_algorithmic_bytes": bb,
+            "bwd_achieved_GBs": bb / tb_med / 1e9, "bwd_frac": bb / tb_med / 1e9 / HBM_PEAK_GBS,
+            "note": "eager autograd (host launch overhead included); backward = "
+                    "action-backward kernels + reduce + exp/ZYZ VJPs"}
 
 
 if __name__ == "__main__":

@@ -11,8 +11,12 @@ the reference step of unsupervised.py:69-117 without its per-step host syncs.  I
 synthetic x ~ U[0,1)^(B x 3 x 64 x 64) resident in HBM (the sphere-cube renders are not
 available offline), seeded per rank.
 
-  python bench_train.py                      # config 3
-  torchrun --nproc-per-node 8 bench_train.py --global-batch 4096    # config 4
+  python bench_train.py                                   # config 3
+  python bench_train.py --gpus 8 --global-batch 4096      # config 4 (spawns 8 ranks)
+  python bench_train.py --gpus 2 --dry-run                # rank plumbing on CPU (gloo)
+
+``--gpus N`` without a torch.distributed environment hands the script to
+torch.distributed.run before any HIP call (lie_vae/experiments/launch.py).
 """
 import argparse
 import json
@@ -24,11 +28,14 @@ import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lie-vae_amd"))
+from lie_vae.experiments import launch  # noqa: E402  (no HIP call at import)
+
 F32_PEAK_TFLOPS = 157.3  # MI355X f32 MFMA = f32 VALU (v_pk_fma_f32) peak, MI355X_MICROARCH.md
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--global-batch", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
@@ -39,17 +46,28 @@ def main():
     ap.add_argument("--no-find", dest="find", action="store_false",
                     help="keep MIOpen's heuristic conv solutions (default: torch.backends."
                          "cudnn.benchmark, MIOpen times the candidates once per shape)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rehearse the rank plumbing on CPU (gloo, no HIP call)")
     args = ap.parse_args()
-    torch.backends.cudnn.benchmark = args.find
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    env = launch.ensure_ranks(args.gpus, os.path.abspath(__file__))
+    world, rank = env.world, env.rank
+    if args.global_batch % world:
+        raise SystemExit(f"global batch {args.global_batch} not divisible by {world} ranks")
     import torch.distributed as dist
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if args.dry_run:
+        launch.init_process_group(env, "gloo")
+        t = torch.tensor([float(rank)])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "rank_sum": float(t.item()),
+                              "per_gpu": args.global_batch // world}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    torch.backends.cudnn.benchmark = args.find
+    launch.init_process_group(env, "nccl")
+    dev = torch.device("cuda", env.local_rank)
     torch.cuda.set_device(dev)
 
     from lie_vae.experiments.train_dp import DPTrainer, param_count

@@ -207,17 +207,32 @@ class _GroupAction(torch.autograd.Function):
         return gang, gspec, None, None, None
 
 
-def group_action(angles, spectrum, L, transpose=False, out_dtype=F32):
-    """block_wigner_matrix_multiply on the HIP path; spectrum (M,C), (n,M,C) or a
-    stride-0 expand of (M,C)."""
-    _lib.require_device(angles, spectrum)
-    n = angles.shape[0]
+def _check_spectrum(spectrum, n, L, what):
+    """The shape contract of block_wigner_matrix_multiply (lie_tools.py:226-253), where
+    the reference's bmm would raise: spectrum (M, C) or (n, M, C) with M = (L+1)^2.  A
+    stride-0 batch expand of (M, C) (ActionNet's item_rep, decoders.py:53) collapses to
+    the shared form.  Checked here because the kernels trust these sizes."""
     M = (L + 1) ** 2
-    C = spectrum.shape[-1]
-    assert spectrum.shape[-2] == M, f"spectrum rows {spectrum.shape[-2]} != (L+1)^2 = {M}"
-    if spectrum.dim() == 3 and spectrum.stride(0) == 0:
-        # (M,C) passed once; autograd routes dF through expand back to item_rep
-        spectrum = spectrum.as_strided(spectrum.shape[1:], spectrum.stride()[1:])
+    assert spectrum.dim() in (2, 3), f"{what}: spectrum must be (M,C) or (n,M,C), " \
+                                     f"got {tuple(spectrum.shape)}"
+    assert spectrum.shape[-2] == M, f"{what}: spectrum rows {spectrum.shape[-2]} != " \
+                                    f"(L+1)^2 = {M}"
+    if spectrum.dim() == 3:
+        assert spectrum.shape[0] == n, f"{what}: spectrum batch {spectrum.shape[0]} != " \
+                                       f"number of samples {n}"
+        if spectrum.stride(0) == 0:
+            # (M,C) passed once; autograd routes dF through expand back to item_rep
+            spectrum = spectrum.as_strided(spectrum.shape[1:], spectrum.stride()[1:])
+    return spectrum
+
+
+def group_action(angles, spectrum, L, transpose=False, out_dtype=F32):
+    """block_wigner_matrix_multiply on the HIP path; angles (n,3), spectrum (M,C),
+    (n,M,C) or a stride-0 expand of (M,C)."""
+    assert angles.dim() == 2 and angles.shape[1] == 3, \
+        f"angles must be (n,3), got {tuple(angles.shape)}"
+    spectrum = _check_spectrum(spectrum, angles.shape[0], L, "group_action")
+    _lib.require_device(angles, spectrum)
     return _GroupAction.apply(angles, _contig(spectrum), L, transpose, out_dtype)
 
 
@@ -274,7 +289,17 @@ class _FusedExpAction(torch.autograd.Function):
 
 
 def fused_exp_action(mu, v, spectrum, L, transpose=False, out_dtype=F32):
-    """(mu (n,3,3) or None, v (n,3), spectrum (M,C) or (n,M,C)) -> (n, M, C)."""
+    """(mu (n,3,3) or None, v (n,3), spectrum (M,C) or a stride-0 expand of it) ->
+    (n, M, C).  The fused kernel takes a shared spectrum only (ActionNet's item_rep);
+    a per-sample spectrum goes through group_action."""
+    assert v.dim() == 2 and v.shape[1] == 3, f"v must be (n,3), got {tuple(v.shape)}"
+    n = v.shape[0]
+    if mu is not None:
+        assert tuple(mu.shape) == (n, 3, 3), f"mu must be ({n},3,3), got {tuple(mu.shape)}"
+    spectrum = _check_spectrum(spectrum, n, L, "fused_exp_action")
+    if spectrum.dim() != 2:
+        raise ValueError("fused_exp_action takes a shared (M,C) spectrum; use group_action "
+                         "for a per-sample (n,M,C) spectrum")
     _lib.require_device(v, spectrum, mu)
     return _FusedExpAction.apply(mu, v, _contig(spectrum), L, transpose, out_dtype)
 

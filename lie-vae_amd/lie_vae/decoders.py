@@ -42,8 +42,23 @@ class ActionNet(nn.Module):
         out = _ops.group_action(angles, self.item_rep, self.degrees, transpose=self.transpose)
         return out.view(-1, self.matrix_dims * self.rep_copies)
 
+    def harmonics_fused(self, mu, v):
+        """The same harmonics for z = mu·exp(v) straight from (mu, v): exp, Euler
+        extraction and the action in ONE launch (lv_fused_exp_action_fwd), instead of
+        so3_sample -> group_matrix_to_eazyz -> group_action (reparameterize.py:269-273,
+        vae.py:182, decoders.py:53-56).  mu (N,3,3) or None (identity), v (N,3)."""
+        out = _ops.fused_exp_action(mu, v, self.item_rep, self.degrees, transpose=self.transpose)
+        return out.view(-1, self.matrix_dims * self.rep_copies)
+
     def forward(self, angles, z_content=None):
         item = self.harmonics(angles)
+        if self.mlp:
+            item = self.mlp(item)
+        return self.deconv(item)
+
+    def forward_fused(self, mu, v):
+        """forward() for z = mu·exp(v) given as (mu, v); see harmonics_fused."""
+        item = self.harmonics_fused(mu, v)
         if self.mlp:
             item = self.mlp(item)
         return self.deconv(item)

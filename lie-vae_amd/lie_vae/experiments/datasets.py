@@ -14,8 +14,8 @@ from ..lie_tools import block_wigner_matrix_multiply, quaternions_to_eazyz, rand
 
 
 def toy_harmonics(degrees=6, rep_copies=10, device=None):
-    """Seeded spectrum ((degrees+1)^2, rep_copies) with norm 10 (datasets.py:145-148)."""
-    torch.manual_seed(0)
+    """Spectrum ((degrees+1)^2, rep_copies) with norm 10, drawn from the CURRENT RNG
+    stream of ``device`` (datasets.py:146-147); the caller seeds (datasets.py:144-145)."""
     h = torch.randn((degrees + 1) ** 2, rep_copies, device=device)
     return h / h.norm() * 10
 
@@ -39,9 +39,11 @@ class ToyDataset(TensorDataset):
     def generate(cls, n=1000, degrees=6, rep_copies=10, device=None, batch_size=64):
         """datasets.py:143-158: seed 0, spectrum first, then one Haar batch of poses per
         ``batch_size`` chunk, each pushed through the fused ZYZ + Wigner-D action."""
+        # One seed, then spectrum and every pose batch from the same device stream, in the
+        # reference's order (datasets.py:144-151): torch.manual_seed(0) seeds the CPU and
+        # every CUDA generator, exactly like the reference's manual_seed + cuda.manual_seed.
+        torch.manual_seed(0)
         harmonics = toy_harmonics(degrees, rep_copies, device)
-        if device is not None and torch.device(device).type == 'cuda':
-            torch.cuda.manual_seed(0)
         xs, qs = [], []
         for i in range(0, n, batch_size):
             batch_n = min(i + batch_size, n) - i

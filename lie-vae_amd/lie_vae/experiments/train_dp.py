@@ -20,6 +20,7 @@ No host synchronisation inside the step: loss terms stay on the device.
 """
 import math
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -87,32 +88,100 @@ class BucketedAllReduce:
         return torch.sqrt(sum(st["buf"].double().square().sum() for st in self.state))
 
 
+class ConstantSchedule:
+    """beta(it) = value (experiments/utils.py ConstantSchedule)."""
+
+    def __init__(self, value):
+        self.value = value
+
+    def __call__(self, it):
+        return self.value
+
+
+class LinearSchedule:
+    """Linear ramp from (start_x, start_y) to (end_x, end_y), clipped to the y range
+    (experiments/utils.py:60-71, same arithmetic: np.clip of the line)."""
+
+    def __init__(self, start_y, end_y, start_x, end_x):
+        self.min_y = min(start_y, end_y)
+        self.max_y = max(start_y, end_y)
+        self.start_x = start_x
+        self.start_y = start_y
+        self.coef = (end_y - start_y) / (end_x - start_x)
+
+    def __call__(self, x):
+        return float(np.clip((x - self.start_x) * self.coef + self.start_y,
+                             self.min_y, self.max_y))
+
+
 class DPTrainer:
-    """Sharded-batch training step with the reference's loss, clip and optimizer."""
+    """Sharded-batch training step with the reference's loss, clip and optimizer.
+
+    The step follows ``UnsupervisedExperiment.train`` (unsupervised.py:69-117):
+      * beta = beta_schedule(global_it), global_it counted from 1 (unsupervised.py:77-78);
+        a float is a constant schedule;
+      * beta == 0: reconstruction only, kl = 0 (unsupervised.py:80-83);
+      * control (KL-controlled VAE, unsupervised.py:87-95):
+        p = 1: (recon + control·|beta − kl|).mean(); p = 2: (recon + control·(beta − kl)²).mean();
+      * clip_grad_norm_ over all parameters, or over encoder + rep_group only with
+        ``selective_clip`` (unsupervised.py:110-115) -- here by the GLOBAL norm, since the
+        gradients are already all-reduced;
+      * Adam step.
+    The per-step NaN-KL check (unsupervised.py:97-98) forces a host sync; it is off by
+    default and enabled with ``nan_check=True``.
+    """
 
     def __init__(self, model, lr=1e-3, weight_decay=0.0, clip_grads=1e-5, beta=1.0,
-                 elbo_samples=1, bucket_bytes=32 << 20, group=None, broadcast=True):
+                 elbo_samples=1, bucket_bytes=32 << 20, group=None, broadcast=True,
+                 control=None, control_p=1, selective_clip=False, nan_check=False):
         self.model = model
         self.clip = clip_grads
-        self.beta = beta
+        self.beta_schedule = beta if callable(beta) else ConstantSchedule(beta)
         self.n = elbo_samples
+        if control is not None and control_p not in (1, 2):
+            raise RuntimeError("Wrong control p")
+        self.control, self.control_p = control, control_p
+        self.selective_clip = selective_clip
+        self.nan_check = nan_check
+        self.it = 0
         if dist.is_initialized() and broadcast:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, src=0, group=group)
         self.ar = BucketedAllReduce(model.parameters(), bucket_bytes=bucket_bytes, group=group)
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
 
-    def loss(self, x, eps=None):
-        recon, kl, _ = self.model.elbo(x, n=self.n, eps=eps)
-        return (recon + self.beta * kl).mean(), recon, kl
+    def loss(self, x, eps=None, beta=1.0):
+        if beta == 0:
+            x_recon = self.model.forward(x, self.n, eps=eps)
+            recon = self.model.recon_loss(x_recon, x)
+            kl = torch.zeros_like(recon)
+        else:
+            recon, kl, _ = self.model.elbo(x, n=self.n, eps=eps)
+        if self.control is None:
+            loss = (recon + beta * kl).mean()
+        elif self.control_p == 1:
+            loss = (recon + self.control * torch.abs(beta - kl)).mean()
+        else:
+            loss = (recon + self.control * (beta - kl) ** 2).mean()
+        return loss, recon, kl
+
+    def clip_params(self):
+        if self.selective_clip:
+            return list(self.model.encoder.parameters()) + \
+                list(self.model.rep_group.parameters())
+        return list(self.model.parameters())
 
     def step(self, x, eps=None):
+        self.it += 1
+        beta = self.beta_schedule(self.it)
         self.ar.zero_grad()
-        loss, recon, kl = self.loss(x, eps)
+        loss, recon, kl = self.loss(x, eps, beta)
+        if self.nan_check and torch.isnan(kl).sum():
+            raise RuntimeError("NaN KL")
         loss.backward()
         self.ar.finish()
         if self.clip:
-            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
+            torch.nn.utils.clip_grad_norm_(self.clip_params(), self.clip)
         self.opt.step()
         return loss.detach(), recon.detach(), kl.detach()
 
@@ -147,5 +216,5 @@ def ring_bytes_per_rank(total_bytes, world):
     return 2 * (world - 1) / world * total_bytes if world > 1 else 0.0
 
 
-__all__ = ["BucketedAllReduce", "DPTrainer", "shard", "param_count", "bucket_plan",
+__all__ = ["BucketedAllReduce", "DPTrainer", "ConstantSchedule", "LinearSchedule", "shard", "param_count", "bucket_plan",
            "ring_bytes_per_rank", "math"]

@@ -26,8 +26,11 @@ class VAE(nn.Module):
                  encode_mode='conv', deconv_mode='deconv', rep_copies=10, batch_norm=True,
                  rgb=False, mean_mode='alg', group_reparam_in_dims=10, normal_dims=3,
                  deterministic=False, item_rep=None, wigner_transpose=False, mlp_layers=3,
-                 mlp_hidden=50, mlp_activation=nn.ReLU, fixed_sigma=None):
+                 mlp_hidden=50, mlp_activation=nn.ReLU, fixed_sigma=None, fused_decode=True):
         super().__init__()
+        # decode z = mu·exp(v) with the one-launch fused kernel when z is the latest
+        # SO(3) sample (same function, fewer launches)
+        self.fused_decode = fused_decode
         self.latent_mode = latent_mode
         self.decoder_mode = decoder_mode
         self.r_callback = None
@@ -114,8 +117,23 @@ class VAE(nn.Module):
         log_p_x_z = -self.recon_loss(x_recon, x)
         return (logsumexp(log_p_x_z + log_p_z - log_q_z_x, dim=0) - np.log(n)).mean()
 
+    def _fusable(self, z_pose):
+        """z_pose is the SO(3) sample mu·exp(v) the latent module just drew (not its means),
+        and the decoder is the action decoder: decode it from (mu, v) in one launch."""
+        rep = getattr(self, 'rep_group', None)
+        return (self.fused_decode and self.decoder_mode == 'action'
+                and self.latent_mode == 'so3' and isinstance(rep, SO3reparameterize)
+                and z_pose is rep.z and not rep.return_means and rep.v is not None
+                and rep.v.dim() == 3 and tuple(rep.v.shape[:2]) == tuple(z_pose.shape[:2]))
+
     def decode(self, z_pose, z_content=None):
         batch_dims = z_pose.shape[:2]
+        if self._fusable(z_pose):
+            rep = self.rep_group
+            n, B = batch_dims
+            mu = rep.mu_lie.expand(n, -1, -1, -1).reshape(-1, 3, 3)
+            x_recon = self.decoder.forward_fused(mu, rep.v.reshape(-1, 3))
+            return x_recon.reshape(*batch_dims, *self.out_shape)
         z_pose = z_pose.reshape(-1, *z_pose.shape[2:])
         if self.decoder_mode == 'action':
             if self.latent_mode in ('so3', 'so3f'):

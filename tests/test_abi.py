@@ -97,9 +97,11 @@ def test_toy_dataset_host_side(tmp_path):
     CPU tensors (the action runs only on the HIP path), and save/load round-trips through
     a weights_only torch.load."""
     from lie_vae.experiments.datasets import ToyDataset, toy_harmonics
+    torch.manual_seed(0)
     h = toy_harmonics(6, 10)
     assert h.shape == (49, 10)
     assert torch.allclose(h.norm(), torch.tensor(10.0))
+    torch.manual_seed(0)  # the caller seeds (datasets.py:144-145); same seed, same draw
     assert torch.equal(h, toy_harmonics(6, 10))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ToyDataset.generate(n=8, degrees=6, device="cpu")
@@ -112,3 +114,24 @@ def test_toy_dataset_host_side(tmp_path):
     assert len(back) == 5
     for a, b in zip(ds.tensors, back.tensors):
         assert torch.equal(a, b)
+
+
+def test_spectrum_shape_contract_raises():
+    """A spectrum whose batch, rows or rank disagree with the angles must raise before any
+    kernel runs (the reference's bmm raises there; the kernels trust these sizes)."""
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    ang = torch.randn(6, 3)
+    with pytest.raises(AssertionError, match="batch"):
+        lt.block_wigner_matrix_multiply(ang, torch.randn(4, 16, 2), 3)
+    with pytest.raises(AssertionError, match="rows"):
+        lt.block_wigner_matrix_multiply(ang, torch.randn(6, 15, 2), 3)
+    with pytest.raises(AssertionError, match="angles"):
+        ops.group_action(torch.randn(6, 4), torch.randn(16, 2), 3)
+    with pytest.raises(AssertionError, match="mu"):
+        ops.fused_exp_action(torch.randn(5, 3, 3), torch.randn(6, 3), torch.randn(16, 2), 3)
+    with pytest.raises(ValueError, match="shared"):
+        ops.fused_exp_action(None, torch.randn(6, 3), torch.randn(6, 16, 2), 3)
+    # a stride-0 expand of (M, C) is the shared form (and then hits the device check)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.fused_exp_action(None, torch.randn(6, 3), torch.randn(16, 2).expand(6, -1, -1), 3)

@@ -19,21 +19,29 @@ from lie_vae.experiments import train_dp
 
 
 class TinyVAE(nn.Module):
-    """Stand-in with the VAE's elbo() contract: recon (B,) and kl (B,)."""
+    """Stand-in with the VAE's contract: encoder, rep_group, forward, recon_loss, elbo()
+    returning recon (B,) and kl (B,)."""
 
     def __init__(self):
         super().__init__()
-        self.enc = nn.Sequential(nn.Linear(12, 16), nn.Tanh(), nn.Linear(16, 6))
+        self.encoder = nn.Sequential(nn.Linear(12, 16), nn.Tanh(), nn.Linear(16, 6))
+        self.rep_group = nn.Linear(6, 6)
         self.dec = nn.Linear(3, 12)
         self.unused = nn.Linear(2, 2)  # never gets a gradient: its bucket must still reduce
 
-    def elbo(self, x, n=1, eps=None):
-        h = self.enc(x)
+    def forward(self, x, n=1, eps=None):
+        h = self.rep_group(self.encoder(x))
         mu, logs = h[:, :3], h[:, 3:]
         z = mu + (eps if eps is not None else 0.0) * logs.exp()
-        recon = (self.dec(z) - x).square().sum(-1)
-        kl = 0.5 * (mu.square() + (2 * logs).exp() - 2 * logs - 1).sum(-1)
-        return recon, kl, [kl]
+        self._kl = 0.5 * (mu.square() + (2 * logs).exp() - 2 * logs - 1).sum(-1)
+        return self.dec(z)
+
+    def recon_loss(self, x_recon, x):
+        return (x_recon - x).square().sum(-1)
+
+    def elbo(self, x, n=1, eps=None):
+        x_recon = self.forward(x, n, eps)
+        return self.recon_loss(x_recon, x), self._kl, [self._kl]
 
 
 def _free_port():
@@ -44,12 +52,27 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, outdir, bucket_bytes, clip):
+TRAIN_KW = {
+    "plain": {},
+    "control": {"beta": None, "control": 0.5, "control_p": 2, "selective_clip": True},
+    "control1": {"beta": None, "control": 0.3, "control_p": 1},
+}
+
+
+def _beta(kind):
+    # a ramp that starts at 0 so that step 1 takes the recon-only branch
+    # (unsupervised.py:80-83), then rises (LinearSchedule, experiments/utils.py:60-71)
+    return train_dp.LinearSchedule(0.0, 2.0, 1, 3) if kind != "plain" else 1.0
+
+
+def _worker(rank, world, port, outdir, bucket_bytes, clip, kind="plain"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(100 + rank)  # different init per rank: broadcast must fix it
     model = TinyVAE()
-    tr = train_dp.DPTrainer(model, lr=1e-2, clip_grads=clip, bucket_bytes=bucket_bytes)
+    kw = dict(TRAIN_KW[kind])
+    kw["beta"] = _beta(kind)
+    tr = train_dp.DPTrainer(model, lr=1e-2, clip_grads=clip, bucket_bytes=bucket_bytes, **kw)
     g = torch.Generator().manual_seed(7)
     for _ in range(3):
         xg = torch.randn(8, 12, generator=g)
@@ -60,19 +83,37 @@ def _worker(rank, world, port, outdir, bucket_bytes, clip):
     dist.destroy_process_group()
 
 
-def _single(outdir, clip):
+def _single(outdir, clip, kind="plain"):
+    """The reference step, written out as unsupervised.py:69-117 does it."""
     torch.manual_seed(100)
     model = TinyVAE()
     opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+    kw = TRAIN_KW[kind]
+    sched = _beta(kind)
+    sched = sched if callable(sched) else (lambda it, b=sched: b)
     g = torch.Generator().manual_seed(7)
-    for _ in range(3):
+    for it in range(3):
         xg = torch.randn(8, 12, generator=g)
         eg = torch.randn(8, 3, generator=g)
+        beta = sched(it + 1)
         opt.zero_grad()
-        recon, kl, _ = model.elbo(xg, eps=eg)
-        (recon + kl).mean().backward()
+        if beta == 0:
+            recon = model.recon_loss(model.forward(xg, 1, eg), xg)
+            kl = torch.zeros_like(recon)
+        else:
+            recon, kl, _ = model.elbo(xg, eps=eg)
+        control = kw.get("control")
+        if control is None:
+            loss = (recon + beta * kl).mean()
+        elif kw["control_p"] == 1:
+            loss = (recon + control * torch.abs(beta - kl)).mean()
+        else:
+            loss = (recon + control * (beta - kl) ** 2).mean()
+        loss.backward()
         if clip:
-            torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
+            params = (list(model.encoder.parameters()) + list(model.rep_group.parameters())
+                      if kw.get("selective_clip") else model.parameters())
+            torch.nn.utils.clip_grad_norm_(params, clip)
         opt.step()
     return model.state_dict()
 
@@ -102,3 +143,27 @@ def test_bucket_plan_for_config3_model():
     sizes = train_dp.bucket_plan(m)
     assert sum(sizes) == 4 * n and len(sizes) >= 1
     assert train_dp.ring_bytes_per_rank(4 * n, 8) == pytest.approx(2 * 7 / 8 * 4 * n)
+
+
+@pytest.mark.parametrize("kind,clip", [("control", 1e-1), ("control1", None)])
+def test_dp_world2_reference_step_semantics(kind, clip):
+    """beta schedule (incl. the beta == 0 recon-only step), KL control p in {1, 2} and
+    selective clipping over encoder + rep_group, at world 2 against the single-process
+    reference step."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, port, d, 256, clip, kind), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, "rank0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "rank1.pt"), weights_only=True)
+        ref = _single(d, clip, kind)
+    for k in ref:
+        assert torch.equal(r0[k], r1[k]), f"replicas diverged at {k}"
+        torch.testing.assert_close(r0[k], ref[k], rtol=1e-5, atol=1e-6)
+
+
+def test_linear_schedule_matches_reference_rule():
+    """experiments/utils.py:88-105 test_linear_schedule, restated."""
+    s = train_dp.LinearSchedule(4, 10, 1, 4)
+    assert s(0) == 4 and s(1) == 4 and s(2) == 6 and s(4) == 10 and s(5) == 10
+    s = train_dp.LinearSchedule(10, 4, 1, 4)
+    assert s(0) == 10 and s(2) == 8 and s(5) == 4

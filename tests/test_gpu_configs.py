@@ -1,0 +1,256 @@
+"""GPU parity of BASELINE configurations 3 and 5 and of the remaining callers of the
+boundary (latent mode ``normal``, the MLP decoders, ToyDataset's RNG stream, the fused
+VAE decode), against the CPU oracle (oracle/lie_ref.py) on identical inputs.
+
+Config 5 (l = 20, B = 8192, bf16 out, fp32 recursion): the timed kernel of that bench,
+``lv_fused_exp_action_fwd`` with a bf16 output, checked on every row against the fp32
+oracle at bf16 rounding tolerance, bitwise against its own fp32 output rounded to bf16,
+and through norm preservation and D^T D F = F at full size.
+
+Config 3 (conv VAE, B = 512): the SO(3) part (mean map -> sigma -> v -> z -> Euler ->
+action) at 1e-5 against the oracle fed the GPU encoder's own features, so MIOpen's conv
+numerics (Winograd etc.) do not pollute the hot-path parity; the convs themselves are
+checked against CPU torch at a conv tolerance.  One DPTrainer step at world 1 must be
+finite and repeatable.
+"""
+import copy
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import assert_normwise, assert_parity_fp64, host
+
+pytestmark = pytest.mark.gpu
+
+BF16_TOL = 2.0 ** -9 + 1e-5  # bf16 round-to-nearest (8 significant bits) + fp32 noise
+
+
+# --------------------------------------------------------------------- config 5
+@pytest.mark.parametrize("n", [8192, 1001])
+def test_config5_fused_bf16_l20(gpu_device, n):
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(500 + n)
+    L, C = 20, 10
+    v = torch.randn(n, 3, generator=gen)
+    F = torch.randn((L + 1) ** 2, C, generator=gen)
+    vd, Fd = v.to(gpu_device), F.to(gpu_device)
+    out = ops.fused_exp_action(None, vd, Fd, L, out_dtype=torch.bfloat16)
+    out32 = ops.fused_exp_action(None, vd, Fd, L)
+    assert out.dtype == torch.bfloat16 and out.shape == (n, (L + 1) ** 2, C)
+    # the bf16 kernel is the fp32 chain rounded once (RNE) at the store
+    same = (out == out32.to(torch.bfloat16)).float().mean().item()
+    assert same >= 1 - 1e-6, f"bf16 output differs from rounded fp32 on {1 - same:.2e}"
+    # every row against the fp32 reference pipeline (chunked: the dense l = 20 chain)
+    o = host(out.float())
+    o32 = host(out32)
+    for a in range(0, n, 2048):
+        b = min(n, a + 2048)
+        ref = lie_ref.block_wigner_apply(lie_ref.mat_to_eazyz(lie_ref.so3_exp(v[a:b])),
+                                         F.expand(b - a, -1, -1), L).numpy()
+        assert_normwise(o[a:b], ref, BF16_TOL, what=f"config5 bf16 rows {a}:{b}")
+        if a == 0:
+            ref64 = lie_ref.block_wigner_apply(
+                lie_ref.mat_to_eazyz(lie_ref.so3_exp(v[a:b].double())),
+                F.double().expand(b - a, -1, -1), L).numpy()
+            assert_parity_fp64(o32[a:b], ref, ref64, what="config5 fp32 fused l=20")
+    # size-independent properties: D orthogonal per degree block, D^T D F = F
+    ob = out.float()
+    for l in (0, 7, 20):
+        r0, r1 = l * l, (l + 1) * (l + 1)
+        torch.testing.assert_close(ob[:, r0:r1].norm(dim=1),
+                                   F[r0:r1].norm(dim=0).to(gpu_device).expand(n, -1),
+                                   rtol=4e-3, atol=1e-3)
+    ang = lt.group_matrix_to_eazyz(lt.rodrigues(vd))
+    back = ops.group_action(ang, ob, L, transpose=True)
+    err = (back - Fd).flatten(1).norm(dim=1) / Fd.norm()
+    assert err.max().item() <= 4e-3, err.max().item()
+
+
+# --------------------------------------------------------------------- config 3
+def _capture(module, store, key):
+    return module.register_forward_hook(lambda m, i, o: store.__setitem__(key, (i[0], o)))
+
+
+def test_config3_conv_vae_b512(gpu_device):
+    from lie_vae.experiments.vae import VAE
+    from oracle import lie_ref
+    L, C, B = 10, 10, 512
+    torch.manual_seed(0)
+    cpu = VAE(latent_mode="so3", decoder_mode="action", degrees=L, rep_copies=C, rgb=True,
+              batch_norm=True, deconv_hidden=200, mean_mode="s2s2")
+    with torch.no_grad():  # non-trivial running statistics (eval mode uses them)
+        for m in cpu.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.1, 0.1)
+                m.running_var.uniform_(0.5, 1.5)
+    cpu.eval()
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(B, 3, 64, 64, generator=g)
+    eps = torch.randn(1, B, 3, generator=g)
+    gvae = copy.deepcopy(cpu).to(gpu_device).eval()
+    cap = {}
+    hooks = [_capture(gvae.encoder, cap, "enc"), _capture(gvae.decoder.deconv, cap, "dec")]
+    with torch.no_grad():
+        recon, kl, _ = gvae.elbo(x.to(gpu_device), 1, eps=eps.to(gpu_device))
+    for h in hooks:
+        h.remove()
+    h_gpu = cap["enc"][1].cpu()
+    harm_gpu = cap["dec"][0].cpu()
+    xr_gpu = cap["dec"][1].cpu()
+    # (1) the encoder convs vs CPU torch (conv tolerance), on a 64-sample slice
+    with torch.no_grad():
+        h_cpu = cpu.encoder(x[:64])
+    assert_normwise(h_gpu[:64].numpy(), h_cpu.numpy(), 1e-4, what="encoder (MIOpen vs CPU)")
+    # (2) the SO(3) hot path at 1e-5, oracle fed the GPU features
+    rep = cpu.rep_group
+    with torch.no_grad():
+        def pipeline(h, e, dt):
+            m6 = rep.mean_module.map.to(dt)(h.to(dt)).double().view(-1, 2, 3)
+            mu = lie_ref.gram_schmidt_s2s2(m6[:, 0], m6[:, 1]).to(dt)
+            sig = lie_ref.n0_sigma(rep.reparameterize.sigma_linear.to(dt)(h.to(dt)))
+            vv = lie_ref.n0_sample(sig, e.to(dt))
+            z = lie_ref.so3_sample(mu, vv)
+            ang = lie_ref.mat_to_eazyz(z.reshape(-1, 3, 3))
+            harm = lie_ref.action_decode(ang, cpu.decoder.item_rep.to(dt), L)
+            lq = lie_ref.so3_log_posterior(vv, sig, 10)
+            return harm, (lq + math.log(8 * math.pi ** 2)).mean(0)
+        harm32, kl32 = pipeline(h_gpu, eps, torch.float32)
+        harm64, _ = pipeline(h_gpu, eps, torch.float64)
+        rep.float()
+    assert_parity_fp64(harm_gpu.numpy(), harm32.numpy(), harm64.numpy(),
+                       what="config3 SO(3) path (s2s2 mean, fused decode)")
+    np.testing.assert_allclose(host(kl), kl32.numpy(), rtol=1e-5, atol=1e-4)
+    # (3) the deconv vs CPU torch on the same harmonics, and the summed-squares recon
+    with torch.no_grad():
+        xr_cpu = cpu.decoder.deconv(harm_gpu[:64])
+    assert_normwise(xr_gpu[:64].numpy().reshape(64, -1), xr_cpu.numpy().reshape(64, -1), 1e-4,
+                    what="deconv (MIOpen vs CPU)")
+    rec_ref = ((xr_gpu - x) ** 2).sum((-1, -2, -3))
+    np.testing.assert_allclose(host(recon).reshape(-1), rec_ref.numpy(), rtol=1e-4)
+
+
+def test_config3_dp_trainer_step_world1(gpu_device):
+    """One data-parallel trainer step (world 1, reference loss, global-norm clip 1e-5,
+    Adam) on the config-3 model: finite, and the same twice from the same state."""
+    from lie_vae.experiments.train_dp import DPTrainer
+    from lie_vae.experiments.vae import VAE
+    torch.manual_seed(0)
+    base = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10, rgb=True,
+               batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(gpu_device)
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(512, 3, 64, 64, generator=g).to(gpu_device)
+    eps = torch.randn(1, 512, 3, generator=g).to(gpu_device)
+    results = []
+    for _ in range(2):
+        m = copy.deepcopy(base)
+        tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5)
+        loss, recon, kl = tr.step(x, eps)
+        loss2, _, _ = tr.step(x, eps)
+        torch.cuda.synchronize()
+        assert torch.isfinite(loss) and torch.isfinite(loss2)
+        assert torch.isfinite(recon).all() and torch.isfinite(kl).all()
+        p = torch.cat([q.detach().flatten() for q in m.parameters()])
+        assert torch.isfinite(p).all()
+        results.append((float(loss), float(loss2), p))
+    assert results[0][0] == pytest.approx(results[1][0], rel=1e-5)
+    assert results[0][1] == pytest.approx(results[1][1], rel=1e-4)
+    torch.testing.assert_close(results[0][2], results[1][2], rtol=1e-4, atol=1e-6)
+
+
+# ------------------------------------------------------ other latent modes / decoders (f4)
+def test_normal_latent_mode_vs_oracle(gpu_device):
+    """latent_mode='normal' + action decoder: Nreparameterize (reparameterize.py:16-55),
+    vector_to_eazyz (lie_tools.py:92-97), ActionNet, injected eps."""
+    from lie_vae.experiments.vae import VAE
+    from oracle import lie_ref
+    L, B, n = 6, 24, 3
+    torch.manual_seed(5)
+    cpu = VAE(latent_mode="normal", decoder_mode="action", degrees=L, encode_mode="toy",
+              deconv_mode="toy", rep_copies=10)
+    x = torch.randn(B, (L + 1) ** 2, 10)
+    eps = torch.randn(n, B, 3)
+    gv = copy.deepcopy(cpu).to(gpu_device)
+    with torch.no_grad():
+        recon, kl, _ = gv.elbo(x.to(gpu_device), n, eps=eps.to(gpu_device))
+        xr = gv.forward(x.to(gpu_device), n, eps=eps.to(gpu_device))
+
+        def pipeline(dt):
+            c = copy.deepcopy(cpu).to(dt)
+            h = c.encoder(x.to(dt))
+            mu = c.rep_group.mu_linear(h)
+            sig = torch.nn.functional.softplus(c.rep_group.sigma_linear(h))
+            z = mu + eps.to(dt) * sig
+            ang = lie_ref.squash_to_eazyz(z.reshape(-1, 3))
+            xr_ref = lie_ref.action_decode(ang, c.decoder.item_rep, L)
+            kl_ref = -0.5 * torch.sum(1 + 2 * sig.log() - mu.pow(2) - sig ** 2, -1)
+            return xr_ref, kl_ref
+        xr32, kl32 = pipeline(torch.float32)
+        xr64, _ = pipeline(torch.float64)
+    assert_parity_fp64(host(xr).reshape(n * B, -1), xr32.numpy(), xr64.numpy(),
+                       what="normal mode x_recon")
+    np.testing.assert_allclose(host(kl), kl32.numpy(), rtol=1e-5, atol=1e-5)
+    rec_ref = ((xr32.reshape(n, B, -1) - x.reshape(1, B, -1)) ** 2).sum(-1)
+    np.testing.assert_allclose(host(recon), rec_ref.numpy(), rtol=1e-4)
+
+
+def test_mlp_decoders_vs_oracle(gpu_device):
+    """MLPNet (decoders.py:64-87) and ActionNet(with_mlp=True) (decoders.py:39-41,58-59)."""
+    from lie_vae.decoders import ActionNet, MLPNet
+    from oracle import lie_ref
+    L, N = 5, 40
+    torch.manual_seed(8)
+    an = ActionNet(L, torch.nn.Sequential(), rep_copies=4, with_mlp=True)
+    mn = MLPNet(L, torch.nn.Sequential(), in_dims=9, rep_copies=4)
+    ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(N))
+    zmat = lie_ref.haar_matrices(N)
+    with torch.no_grad():
+        ya = copy.deepcopy(an).to(gpu_device)(ang.to(gpu_device))
+        ym = copy.deepcopy(mn).to(gpu_device)(zmat.to(gpu_device))
+        ref_a = an.mlp(lie_ref.action_decode(ang, an.item_rep, L))
+        ref_m = mn.mlp(zmat.reshape(N, -1))
+    assert_normwise(host(ya), ref_a.numpy(), 1e-5, what="ActionNet(with_mlp)")
+    assert_normwise(host(ym), ref_m.numpy(), 1e-5, what="MLPNet")
+
+
+def test_toy_dataset_reference_rng_stream(gpu_device):
+    """ToyDataset.generate draws the spectrum and every pose batch from ONE seeded device
+    stream, in the reference's order (datasets.py:144-151): replay that order with plain
+    torch on the same device and compare bit for bit."""
+    from lie_vae.experiments.datasets import ToyDataset
+    from lie_vae.lie_tools import random_quaternions
+    n, deg, C, bs = 150, 6, 10, 64
+    ds = ToyDataset.generate(n=n, degrees=deg, rep_copies=C, device=gpu_device, batch_size=bs)
+    torch.manual_seed(0)
+    torch.cuda.manual_seed(0)
+    h = torch.randn((deg + 1) ** 2, C, device=gpu_device)
+    h = h / h.norm() * 10
+    qs = [random_quaternions(min(i + bs, n) - i, device=gpu_device) for i in range(0, n, bs)]
+    assert torch.equal(ds.tensors[1][0], h)
+    assert torch.equal(ds.tensors[0], torch.cat(qs, 0))
+
+
+def test_vae_fused_decode_matches_modular(gpu_device):
+    """VAE.decode's one-launch path (z = mu·exp(v) -> action) against the modular path
+    (so3_sample -> group_matrix_to_eazyz -> ActionNet), outputs and every gradient."""
+    from lie_vae.experiments.vae import VAE
+    L, B, n = 8, 64, 2
+    torch.manual_seed(4)
+    a = VAE(latent_mode="so3", decoder_mode="action", degrees=L, encode_mode="toy",
+            deconv_mode="toy", rep_copies=10, mean_mode="q").to(gpu_device)
+    b = copy.deepcopy(a)
+    b.fused_decode = False
+    x = torch.randn(B, (L + 1) ** 2, 10, device=gpu_device)
+    eps = torch.randn(n, B, 3, device=gpu_device)
+    outs = []
+    for m in (a, b):
+        recon, kl, _ = m.elbo(x, n, eps=eps)
+        (recon.sum() + kl.sum()).backward()
+        outs.append((recon.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-5, atol=1e-4)
+    for k in outs[0][1]:
+        assert_normwise(host(outs[0][1][k]).reshape(1, -1), host(outs[1][1][k]).reshape(1, -1),
+                        1e-4, what=f"grad {k}")
