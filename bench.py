@@ -401,11 +401,64 @@ def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     tbs = sorted(b0.elapsed_time(b1) / 1e3 for b0, b1 in tb)
     tb_med = tbs[len(tbs) // 2]
     bb = algorithmic_bytes_bwd(B, L, C)
+    kern = bench_action_bwd_kernel(vg.detach(), F, gout, L, dev)
     return {"value": B / t, "unit": "samples/s", "us_per_step": t * 1e6,
             "bwd_us_median": tb_med * 1e6, "bwd_algorithmic_bytes": bb,
             "bwd_achieved_GBs": bb / tb_med / 1e9, "bwd_frac": bb / tb_med / 1e9 / HBM_PEAK_GBS,
+            "action_bwd": kern,
             "note": "eager autograd (host launch overhead included); backward = "
-                    "action-backward kernels + reduce + exp/ZYZ VJPs"}
+                    "action-backward kernel + dF reduce + exp/ZYZ VJPs"}
+
+
+def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):
+    """lv_group_action_bwd alone (backward tile kernel + deterministic dF reduce), graph-
+    captured back-to-back calls on resident inputs: the angle/spectrum gradient of
+    block_wigner_matrix_multiply (lie_tools.py:226-253) at the metric size."""
+    import lie_vae._ops as ops
+    from lie_vae import _lib
+    lib = _lib.load()
+    B, C = v.shape[0], F.shape[1]
+    M = (L + 1) ** 2
+    ang = torch.empty(B, 3, device=dev)
+    out = ops.fused_exp_action(None, v, F, L)
+    lib.lv_fused_exp_action_fwd(None, ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(F.data_ptr()), 0,
+                                ctypes.c_void_p(out.data_ptr()), _lib.LV_DTYPE_F32,
+                                ctypes.c_void_p(ang.data_ptr()), B, L, C, 0, None)
+    gang = torch.empty(B, 3, device=dev)
+    gF = torch.empty(M, C, device=dev)
+    ws_bytes = lib.lv_group_action_bwd_workspace(B, L, C, 1)
+    ws = torch.empty(max(ws_bytes, 1), device=dev, dtype=torch.uint8)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    torch.cuda.synchronize(dev)
+    s = torch.cuda.Stream(dev)
+
+    def call(k, st):
+        for _ in range(k):
+            rc = lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0,
+                                         P(ws), ws_bytes, ctypes.c_void_p(st.cuda_stream))
+            if rc:
+                raise RuntimeError(_lib.last_error())
+
+    call(2, s)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        call(50, s)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cur = torch.cuda.current_stream(dev)
+    e0.record(cur)
+    for _ in range(reps // 50):
+        g.replay()
+    e1.record(cur)
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / (reps // 50 * 50)
+    bb = B * (12 + M * C * 4 + 12) + 2 * M * C * 4 + ws_bytes * 2
+    return {"us_per_call": us, "samples_per_s": B / us * 1e6, "bytes_per_call": bb,
+            "achieved_GBs": bb / us / 1e3, "frac": bb / us / 1e3 / HBM_PEAK_GBS,
+            "bytes_note": "angles + output gradient in, angle gradient out, F in / dF out, "
+                          "the dF slabs written and read once (workspace)"}
 
 
 if __name__ == "__main__":

@@ -18,23 +18,39 @@ LV_EXTERN_LAUNCHERS(20)
 LV_EXTERN_BWD(0) LV_EXTERN_BWD(1) LV_EXTERN_BWD(2) LV_EXTERN_BWD(3) LV_EXTERN_BWD(4)
 LV_EXTERN_BWD(5) LV_EXTERN_BWD(6) LV_EXTERN_BWD(7) LV_EXTERN_BWD(8) LV_EXTERN_BWD(9)
 LV_EXTERN_BWD(10) LV_EXTERN_BWD(11) LV_EXTERN_BWD(12) LV_EXTERN_BWD(13) LV_EXTERN_BWD(14)
+LV_EXTERN_BWD(15) LV_EXTERN_BWD(16) LV_EXTERN_BWD(17) LV_EXTERN_BWD(18) LV_EXTERN_BWD(19)
+LV_EXTERN_BWD(20)
 
-__global__ void action_bwd_reduce_kernel(const float* ws_ang, const float* ws_F, float* gang,
-                                         float* gF, int64_t n, int64_t MC, int nseg, int gridX,
-                                         int sharedF) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n * 3) {
-    float sum = 0.f;
-    for (int sg = 0; sg < nseg; ++sg) sum += ws_ang[(int64_t)sg * n * 3 + t];
-    gang[t] = sum;
+// Shared-spectrum gradient: gF[e] = sum over the blocks' slabs in block order.  One block
+// per 64 consecutive elements; its 16 waves each sum a contiguous run of slabs (loads
+// unrolled for memory parallelism), then the 16 partials are added in wave order.
+__global__ __launch_bounds__(64 * kBwdReduceWaves) void action_bwd_reduce_kernel(
+    const float* ws_F, float* gF, int64_t MC, int nslab) {
+  __shared__ float part[kBwdReduceWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int per = (nslab + kBwdReduceWaves - 1) / kBwdReduceWaves;
+  const int b0 = min(nslab, w * per), b1 = min(nslab, b0 + per);
+  float sum = 0.f;
+  if (e < MC) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ws_F[(int64_t)(b + k) * MC + e];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += v[k];
+    }
+    for (; b < b1; ++b) sum += ws_F[(int64_t)b * MC + e];
   }
-  if (sharedF && t < MC) {
-    float sum = 0.f;
-    for (int b = 0; b < gridX; ++b) sum += ws_F[(int64_t)b * MC + t];
-    gF[t] = sum;
+  part[w][lane] = sum;
+  __syncthreads();
+  if (w == 0 && e < MC) {
+    float r = part[0][lane];
+    for (int k = 1; k < kBwdReduceWaves; ++k) r += part[k][lane];
+    gF[e] = r;
   }
 }
-
 
 namespace {
 
@@ -96,23 +112,18 @@ constexpr double kPrologueFwd = 200.0;
 constexpr double kPrologueFused = 250.0;
 
 // Tile kernel (shared spectrum): one block per sample group, one wave per degree
-// segment, output staged in LDS and written as whole lines.  Measured on MI355X
-// (tools/tilebench.hip, l = 10, C = 10): 5 segments best at batch 4096, 4 at 65536;
-// write-through (sc1) stores best while the output is small enough to be written during
-// the kernel (batch 4096, 19.8 MB: 7.4 vs 8.3 us nt), nt beyond (65536: 77 vs 93 us).
-constexpr size_t kTileMaxLds = 64 * 1024;  // >= 2 blocks per CU (l = 20 bf16 ran 53 vs 43 us at 85 KB)
-constexpr double kTileSegCostSmall = 450.0;   // per-wave chain cost target, few groups
-constexpr double kTileSegCostLarge = 560.0;   // ... many groups (>= kTileManyGroups)
+// segment, the prologue once per (sample, slot), output staged in LDS and written as
+// whole lines.  Measured on MI355X (tools/fwdbench.hip, l = 10, C = 10,
+// profiles/r02_fwd_ab_*.txt): 6-8 segments best at batch 4096, 4 at 65536 (fewer
+// segments = fewer waves to hide the chain latency, more = more spectrum staging and a
+// bigger block); write-through (sc1) stores best while the output is small enough to be
+// written during the kernel (batch 4096, 19.8 MB), nt beyond (65536: 68 vs 81 us).
+constexpr size_t kTileMaxLds = 80 * 1024;    // >= 2 blocks per CU
+constexpr double kTileSegCostSmall = 340.0;  // per-wave chain cost target, few groups
+constexpr double kTileSegCostLarge = 560.0;  // ... many groups (>= kTileManyGroups)
+constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
-// Paired-column tile kernel (C = 10, l <= kPairMaxL): 12 samples per block; its tile is
-// twice as large, so up to 80 KB of LDS (still 2 blocks per CU).  OFF by default: it is
-// bit-identical to the scalar tile kernel but measured slower on MI355X (B = 4,096:
-// 7.94 vs 7.38 us; 65,536: 79.7 vs 74.6 us, best segment count each) -- halving the VALU
-// stream does not pay, the kernel is bound by latency and the store path, not VALU issue
-// (DESIGN.md section 9).  LV_TILE_PAIR=1 enables it, LV_PAIR_NSEG=k sets its segment count.
-constexpr size_t kTilePairMaxLds = 80 * 1024;
-constexpr int kPairSegDefault = 7;
 
 // LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy (A/B
 // testing and diagnosis only; read once per process).
@@ -121,34 +132,32 @@ int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 
-bool plan_tile(FwdLaunch& p, int L, int out_bytes, bool pair) {
+bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvTile = env_int("LV_TILE", 1);
   static const int kEnvWT = env_int("LV_TILE_WT", -1);
-  static const int kEnvPairSeg = env_int("LV_PAIR_NSEG", 0);
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
-  a.Sw = pair ? kPairSw : 64 / a.C;
-  const int64_t groups = (a.n + a.Sw - 1) / a.Sw;
+  const int Sw = 64 / a.C;
+  const int64_t groups = (a.n + Sw - 1) / Sw;
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
   const double target = groups < kTileManyGroups ? kTileSegCostSmall : kTileSegCostLarge;
   int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
-  if (pair) nseg = std::min(L + 1, kEnvPairSeg > 0 ? std::min(8, kEnvPairSeg) : kPairSegDefault);
-  plan_segments(L, nseg, kPrologueFused, false, a.seg_lo);
+  // the prologue takes one thread per (sample, slot): 3*Sw threads of the block
+  nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
+  if (3 * Sw > 64 * nseg || nseg > 8) return false;
+  plan_segments(L, nseg, kTilePrologue, false, a.seg_lo);
   int fp = 0;
   for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
   a.fpitch = (fp + 3) & ~3;
-  const size_t trig = pair ? (size_t)a.Sw * (6 * ((L + 1 + 3) & ~3) + 4) : 0;  // TrigLds<L>::kRow
-  const size_t lds = (size_t)tile_stage_bytes(a.Sw, a.MC, out_bytes) +
+  const size_t trig = (size_t)Sw * (6 * ((L + 1 + 3) & ~3) + 4);  // TrigLds<L>::kRow per sample
+  const size_t lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) +
                      sizeof(float) * ((size_t)nseg * a.fpitch + trig);
-  if (lds > (pair ? kTilePairMaxLds : kTileMaxLds) || groups > 0x7fffffff) {
-    a.Sw = 64 / a.C;
-    return false;
-  }
+  if (lds > kTileMaxLds || groups > 0x7fffffff) return false;
+  a.Sw = Sw;
   a.write_through = (int64_t)a.n * a.MC * out_bytes <= kWriteThroughMaxBytes ? 1 : 0;
   if (kEnvWT >= 0) a.write_through = kEnvWT;
   p.tile = true;
-  p.pair = pair;
   p.lds = lds;
   p.gx = (int)groups;
   p.gy = nseg;
@@ -202,11 +211,8 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   p.fused = fused;
   p.dtype = out_dtype;
   p.stream = stream;
-  static const int kEnvPair = env_int("LV_TILE_PAIR", 0);
   const int ob = out_dtype == LV_DTYPE_BF16 ? 2 : 4;
-  if (Fstride == 0 && kEnvPair && C == kPairC && L <= kPairMaxL && plan_tile(p, L, ob, true))
-    return dispatch_L<FwdLauncher>(L, p);
-  if (Fstride == 0 && plan_tile(p, L, ob, false))
+  if (Fstride == 0 && plan_tile(p, L, ob))
     return dispatch_L<FwdLauncher>(L, p);
   const double P = fused ? kPrologueFused : kPrologueFwd;
   const int nseg = choose_nseg(n, p.a.Sw, L, P, false);
@@ -226,26 +232,56 @@ template <template <int> class Launcher, class Args, int... Is>
 constexpr std::array<int (*)(Args&), sizeof...(Is)> launcher_table(std::integer_sequence<int, Is...>) {
   return {&Launcher<Is>::run...};
 }
-constexpr auto kBwdRun = launcher_table<BwdLauncher, BwdLaunch>(std::make_integer_sequence<int, kNumBwdRanges>{});
+constexpr auto kBwdRun = launcher_table<BwdLauncher, BwdLaunch>(std::make_integer_sequence<int, LV_MAX_DEGREE + 1>{});
 constexpr auto kWigRun = launcher_table<WigLauncher, WigLaunch>(std::make_integer_sequence<int, LV_MAX_DEGREE + 1>{});
-static_assert(bwd_range_hi(kNumBwdRanges - 1) == LV_MAX_DEGREE + 1, "backward ranges must cover l_max");
+
+// Backward plan (action_bwd_tile_kernel): samples per block (Sw <= 64/C, reduced until the
+// fp32 gradient tile fits), degree segments as in the forward (the backward chain costs
+// ~2.2x), grid capped at kBwdMaxBlocks so the dF workspace stays bounded (blocks then
+// loop over groups).
+constexpr size_t kBwdMaxLds = 96 * 1024;
+constexpr int64_t kBwdMaxBlocks = 4096;
+constexpr double kBwdSegCostSmall = 2.2 * 340.0;
+constexpr double kBwdSegCostLarge = 2.2 * 560.0;
 
 struct BwdPlan {
-  int nr, gx, groups, Sw;
-  size_t ws_ang, ws_F;
+  int Sw, nseg, gx, fpitch;
+  int64_t groups;
+  int seg_lo[kMaxSeg + 1];
+  size_t lds, ws;
 };
 
-BwdPlan plan_bwd(int64_t n, int L, int C, bool sharedF) {
-  BwdPlan b{};
-  b.Sw = 64 / C;
-  b.nr = bwd_num_ranges(L);
-  b.groups = (int)((n + (int64_t)b.Sw * kWavesPerBlock - 1) / ((int64_t)b.Sw * kWavesPerBlock));
-  // bound the slab count: each block walks several sample groups
-  b.gx = std::max(1, std::min(b.groups, sharedF ? 512 : 1 << 30));
-  b.ws_ang = sizeof(float) * (size_t)b.nr * (size_t)n * 3;
-  const size_t MC = (size_t)(L + 1) * (L + 1) * C;
-  b.ws_F = sharedF ? sizeof(float) * (size_t)b.gx * MC : 0;
-  return b;
+bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
+  static const int kEnvNseg = env_int("LV_BWD_NSEG", 0);  // A/B testing only
+  b = BwdPlan{};
+  const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
+  double total = 0.0;
+  for (int l = 0; l <= L; ++l) total += degree_cost(l, true);
+  for (int Sw = 64 / C; Sw >= 1; --Sw) {
+    const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
+    const double target = groups < kTileManyGroups ? kBwdSegCostSmall : kBwdSegCostLarge;
+    int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
+    if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
+    nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
+    if (3 * Sw > 64 * nseg || nseg > 8) continue;
+    plan_segments(L, nseg, kTilePrologue, true, b.seg_lo);
+    int fp = 0;
+    if (sharedF)
+      for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(b.seg_lo[k], b.seg_lo[k + 1]) * C);
+    b.fpitch = (fp + 3) & ~3;
+    const size_t lds = (size_t)tile_stage_bytes(Sw, MC, 4) +
+                       sizeof(float) * ((size_t)bwd_trig_floats(Sw, L) + (size_t)nseg * 64 * 3 +
+                                        (sharedF ? (size_t)MC : 0) + (size_t)nseg * b.fpitch);
+    if (lds > kBwdMaxLds) continue;
+    b.Sw = Sw;
+    b.nseg = nseg;
+    b.groups = groups;
+    b.gx = (int)std::min<int64_t>(groups, kBwdMaxBlocks);
+    b.lds = lds;
+    b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)MC : 0;
+    return true;
+  }
+  return false;
 }
 
 }  // namespace
@@ -282,8 +318,9 @@ int lv_fused_exp_action_fwd_repeat(const float* mu, const float* v, const float*
 
 size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F) {
   if (n <= 0 || L < 0 || L > LV_MAX_DEGREE || C < 1 || C > LV_MAX_CHANNELS) return 0;
-  const BwdPlan b = plan_bwd(n, L, C, shared_F != 0);
-  return b.ws_ang + b.ws_F;
+  BwdPlan b;
+  if (!plan_bwd(n, L, C, shared_F != 0, b)) return 0;
+  return b.ws;
 }
 
 int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride,
@@ -300,9 +337,10 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
     return LV_OK;
   }
   LV_CHECK_ARG(ang && F && gout && gang && gF, "null pointer argument");
-  const BwdPlan b = plan_bwd(n, L, C, sharedF);
-  if (ws_bytes < b.ws_ang + b.ws_F || !workspace) {
-    set_error("workspace too small: need %zu bytes", b.ws_ang + b.ws_F);
+  BwdPlan b;
+  LV_CHECK_ARG(plan_bwd(n, L, C, sharedF, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
+  if (sharedF && (ws_bytes < b.ws || !workspace)) {
+    set_error("workspace too small: need %zu bytes", b.ws);
     return LV_ERR_WORKSPACE;
   }
   BwdLaunch p{};
@@ -310,27 +348,25 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
   p.a.F = F;
   p.a.Fstride = F_batch_stride;
   p.a.gout = gout;
+  p.a.gang = gang;
   p.a.gF = gF;
-  p.a.ws_ang = (float*)workspace;
-  p.a.ws_F = (float*)((char*)workspace + b.ws_ang);
+  p.a.ws_F = (float*)workspace;
   p.a.n = n;
   p.a.MC = MC;
+  p.a.groups = b.groups;
   p.a.C = C;
   p.a.Sw = b.Sw;
   p.a.transpose = transpose ? 1 : 0;
-  p.a.groups = b.groups;
-  p.a.L = L;
+  p.a.fpitch = b.fpitch;
+  for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
   p.gx = b.gx;
+  p.nseg = b.nseg;
+  p.lds = b.lds;
   p.stream = st;
-  for (int r = 0; r < b.nr; ++r) {
-    const size_t lds = sizeof(float) * kWavesPerBlock * (size_t)bwd_wave_floats(r, L, C, sharedF);
-    LV_CHECK_ARG(lds <= 160 * 1024, "LDS plan too large (%zu B)", lds);
-    p.a.slot = r;
-    if (int e = kBwdRun[r](p)) return e;
-  }
-  const int64_t work = std::max<int64_t>(n * 3, sharedF ? MC : 0);
-  hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(work, 256)), dim3(256), 0, st,
-                     p.a.ws_ang, p.a.ws_F, gang, gF, n, MC, b.nr, b.gx, sharedF ? 1 : 0);
+  if (int e = kBwdRun[L](p)) return e;
+  if (!sharedF) return LV_OK;
+  hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, 64)), dim3(64 * kBwdReduceWaves),
+                     0, st, (const float*)workspace, gF, MC, b.gx);
   LV_RETURN_LAUNCH("action_bwd_reduce_kernel");
 }
 

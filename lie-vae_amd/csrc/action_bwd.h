@@ -1,217 +1,352 @@
 #pragma once
-// Backward of the group action (angles + spectrum gradients) for gfx950, one kernel
-// per fixed degree range (action_bwd_inst.hip, -DLV_BWD_R=r), plus its launcher.
-#include "action_common.h"
+// Backward of the group action (angle + spectrum gradients) for gfx950, instantiated once
+// per l_max in action_bwd_inst.hip (-DLV_INST_L=k), plus the deterministic reduction of
+// the shared-spectrum gradient.  The reference gets these from autograd through
+// lie_tools.py:211-253 (wigner_d_matrix, block_wigner_matrix_multiply).
+#include "action_fwd.h"
 
 namespace lv {
 
 // ---------------------------------------------------------------- backward
-// Per lane (sample, column), per degree, with G = gout block column:
+// Same decomposition as the forward tile kernel: one block per group of Sw samples, one
+// wave per degree segment.  The group's upstream gradient (Sw*M*C contiguous values) is
+// loaded into an LDS tile with 16-byte loads issued first thing; the per-sample
+// prologue (sincos of the three angles, multiples by recurrence) runs once per
+// (sample, slot) into an LDS table.  Per lane (sample, column), per degree, with
+// G = gout block column:
 //   P1 = Xc F, P2 = J P1, P3 = Xb P2, P4 = J P3           (forward recompute)
 //   Q4 = Xa^T G, Q3 = J Q4, Q2 = Xb^T Q3, Q1 = J Q2, dF = Xc^T Q1
 //   d/da = <G, Xa' P4>, d/db = <Q3, Xb' P2>, d/dc = <Q1, Xc' F>
-// Angle partials are summed over the C lanes of a sample in LDS (fixed order) and
-// written per segment to the workspace; dF is summed over the wave's samples and its
-// grid-stride loop into a per-wave LDS accumulator, then per block into a slab.
-// A second kernel reduces slabs and segments in a fixed order (bitwise reproducible).
+// The dF column overwrites the lane's own G values in the tile (each degree's rows
+// belong to one wave).  Angle gradients: the C lanes of a sample and the segment waves
+// are summed in a fixed order in LDS and written straight to gang.  dF: per-sample
+// spectrum -> the tile leaves as gF with one contiguous flush; shared spectrum -> each
+// wave sums its rows over the group's samples (fixed order) into the block's LDS slab;
+// blocks loop over groups (grid capped so the workspace stays
+// bounded), write their slab to the workspace once, and action_bwd_reduce_kernel sums
+// the slabs in block order.  No atomics: bitwise reproducible.
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
   int64_t Fstride;
   const float* gout;
+  float* gang;
   float* gF;           // per-sample spectrum: written directly
-  float* ws_ang;       // [nranges][n][3]
-  float* ws_F;         // [gridX][M*C] (shared F only)
+  float* ws_F;         // [gridDim.x][M*C] (shared F only)
   int64_t n;
   int64_t MC;
-  int C, Sw, transpose, groups, L, slot;
+  int64_t groups;      // ceil(n / Sw); block b takes groups b, b + gridDim.x, ...
+  int C, Sw, transpose;
+  int fpitch;          // floats per wave-private spectrum slice in LDS
+  int seg_lo[kMaxSeg + 1];
 };
 
-// Degree ranges of the backward, fixed at compile time and shared by every l_max:
-// [0,6) [6,8) then one degree per range up to 20.  Each range is its own kernel (small
-// functions: fast to compile, registers sized to the range), launched one after another;
-// the range containing l_max is clipped at run time.
-constexpr int kNumBwdRanges = 15;
-__host__ __device__ constexpr int bwd_range_lo(int r) { return r == 0 ? 0 : (r == 1 ? 6 : r + 6); }
-__host__ __device__ constexpr int bwd_range_hi(int r) { return r == 0 ? 6 : (r == 1 ? 8 : r + 7); }
-inline int bwd_num_ranges(int L) {
-  int n = 0;
-  while (n < kNumBwdRanges && bwd_range_lo(n) <= L) ++n;
-  return n;
-}
-inline int bwd_wave_floats(int r, int L, int C, bool sharedF) {
-  const int hi = bwd_range_hi(r) < L + 1 ? bwd_range_hi(r) : L + 1;
-  const int lo = bwd_range_lo(r);
-  const int LT = bwd_range_hi(r) - 1;
-  return 64 * (2 * LT + 1) + 64 * 3 + (sharedF ? (hi * hi - lo * lo) * C : 0);
+// LDS floats of the backward tile kernel beyond the gout tile.
+__host__ __device__ inline int bwd_trig_floats(int Sw, int L) {
+  return Sw * (6 * ((L + 1 + 3) & ~3) + 4);  // TrigLds<L>::kRow per sample
 }
 
-template <int R>
-__global__ __launch_bounds__(kThreads) void action_bwd_kernel(ActionBwdArgs a) {
-  constexpr int LO = bwd_range_lo(R), HI = bwd_range_hi(R), LT = HI - 1;
-  extern __shared__ float lds[];
+// One Euler slot's multiples for degree l (f <= l), fetched from the LDS table with
+// 16-byte reads right before use, so that at most one slot's are live in registers.
+template <int l>
+struct Mult {
+  float c[l + 1], s[l + 1];
+};
+template <int l, int A, int LT>
+__device__ __forceinline__ Mult<l> mult_lds(const float* tj) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int TP = TrigLds<LT>::TP;
+  Mult<l> m;
+  sfor<(l + 4) / 4>([&](auto K) {
+    constexpr int k4 = LV_CV(K);
+    const f4 cv = *reinterpret_cast<const f4*>(tj + 2 * A * TP + 4 * k4);
+    const f4 sv = *reinterpret_cast<const f4*>(tj + (2 * A + 1) * TP + 4 * k4);
+    sfor<4>([&](auto I) {
+      constexpr int f = 4 * k4 + LV_CV(I);
+      if constexpr (f <= l) {
+        m.c[f] = cv[LV_CV(I)];
+        m.s[f] = sv[LV_CV(I)];
+      }
+    });
+  });
+  return m;
+}
+// y = X x, y = X^T x and <g, X' x> on one slot's multiples (the arithmetic of xrot,
+// xrot_t and xrot_dot_deriv in action_chain.h, operation for operation).
+template <int l>
+__device__ __forceinline__ void xm(const Mult<l>& m, const float (&x)[2 * l + 1], float (&y)[2 * l + 1]) {
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) y[i] = x[i];
+    else if constexpr (f > 0) y[i] = fmaf(m.c[f], x[i], m.s[f] * x[2 * l - i]);
+    else y[i] = fmaf(m.c[-f], x[i], -(m.s[-f] * x[2 * l - i]));
+  });
+}
+template <int l>
+__device__ __forceinline__ void xm_t(const Mult<l>& m, const float (&x)[2 * l + 1], float (&y)[2 * l + 1]) {
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f == 0) y[i] = x[i];
+    else if constexpr (f > 0) y[i] = fmaf(m.c[f], x[i], -(m.s[f] * x[2 * l - i]));
+    else y[i] = fmaf(m.c[-f], x[i], m.s[-f] * x[2 * l - i]);
+  });
+}
+template <int l>
+__device__ __forceinline__ float xm_dd(const Mult<l>& m, const float (&g)[2 * l + 1], const float (&x)[2 * l + 1]) {
+  float acc = 0.f;
+  sfor<2 * l + 1>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    if constexpr (f > 0) {
+      const float d = fmaf(-m.s[f], x[i], m.c[f] * x[2 * l - i]);
+      acc = fmaf(g[i], (float)f * d, acc);
+    } else if constexpr (f < 0) {
+      const float d = fmaf(m.s[-f], x[i], m.c[-f] * x[2 * l - i]);
+      acc = fmaf(g[i], (float)f * d, acc);
+    }
+  });
+  return acc;
+}
+
+// Upstream-gradient tile fill: global -> registers (16-byte loads, issued before the
+// prologue so their latency overlaps it) -> LDS.  Same head/body/tail split as
+// tile_flush; the LDS tile starts `mis` bytes past a 16-B boundary.
+constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per thread
+
+template <int LT, int CT, bool SHAREDF>
+__global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int kRow = TrigLds<LT>::kRow;
+  const int C = CT > 0 ? CT : a.C;
+  const int Sw = a.Sw;
+  const int64_t MC = CT > 0 ? (int64_t)(LT + 1) * (LT + 1) * CT : a.MC;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int C = a.C, Sw = a.Sw;
+  const int tid = (int)threadIdx.x, nthr = (int)blockDim.x;
   const int j = lane / C;
   const int c = lane - j * C;
-  const int lo = LO, hi = min(HI, a.L + 1);
-  const bool sharedF = a.Fstride == 0;
-  const int rows_lo = lo * lo, rows_hi = hi * hi;
-  const int seg_len = (rows_hi - rows_lo) * C;
-  // LDS: per wave [stage 64*(2LT+1)] [angle partials 64*3] [dF accumulator seg_len]
-  const int wave_floats = 64 * (2 * LT + 1) + 64 * 3 + (sharedF ? seg_len : 0);
-  float* stage = lds + wave * wave_floats;
-  float* apart = stage + 64 * (2 * LT + 1);
-  float* facc = apart + 64 * 3;
-  if (sharedF)
-    for (int e = lane; e < seg_len; e += 64) facc[e] = 0.f;
-  wave_lds_sync();
-
-  for (int g = blockIdx.x; g < a.groups; g += gridDim.x) {
-    const int64_t s0 = ((int64_t)g * kWavesPerBlock + wave) * Sw;
-    if (s0 >= a.n) break;
-    const int Sv = (int)min((int64_t)Sw, a.n - s0);
-    const int64_t s = s0 + j;
-    const bool active = j < Sv;
-    float cc[3] = {1.f, 1.f, 1.f}, ss[3] = {0.f, 0.f, 0.f};
-    if (active)
-      for (int i = 0; i < 3; ++i) sincosf(a.ang[s * 3 + i], &ss[i], &cc[i]);
-    float c1[3], s1[3];
-    if (a.transpose) {
-      c1[0] = cc[2]; s1[0] = -ss[2];
-      c1[1] = cc[1]; s1[1] = -ss[1];
-      c1[2] = cc[0]; s1[2] = -ss[0];
-    } else {
-      for (int i = 0; i < 3; ++i) { c1[i] = cc[i]; s1[i] = ss[i]; }
+  const int lo = a.seg_lo[wave], hi = a.seg_lo[wave + 1];
+  const int rows_lo = lo * lo;
+  const int frows = fseg_rows(lo, hi);
+  const int stage_bytes = tile_stage_bytes(Sw, MC, 4);
+  // LDS: [gout / dF tile][multiples table][angle partials][dF slab (shared F)][F slices]
+  float* trig = lds + (stage_bytes >> 2);
+  float* apart = trig + bwd_trig_floats(Sw, LT);               // [nseg][64][3]
+  float* slabL = apart + (nthr >> 6) * 64 * 3;                 // [M*C] (shared F)
+  float* Fw = slabL + (SHAREDF ? (int)MC : 0) + wave * a.fpitch;
+  // spectrum slice (shared F): once per block
+  constexpr int kFPer = 6;
+  const int fcnt = SHAREDF ? (hi * hi - rows_lo) * C : 0;
+  const float* fsrc = a.F + rows_lo * C;
+  if constexpr (SHAREDF) {
+    float fv[kFPer];
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+      const int e = lane + 64 * k;
+      fv[k] = e < fcnt ? fsrc[e] : 0.f;
     }
-    TrigTab<LT> t;
-    trig_fill<LT>(t, c1, s1, hi - 1);
-    float ga = 0.f, gb = 0.f, gc = 0.f;
-    const float* Fbase = a.F + (active ? s * a.Fstride : 0) + c;
+    for (int e = lane; e < fcnt; e += 64) slabL[rows_lo * C + e] = 0.f;  // this wave's rows
+    if constexpr (CT > 0) {
+#pragma unroll
+      for (int k = 0; k < kFPer; ++k) {
+        const int e = lane + 64 * k;
+        if (e < fcnt) Fw[e] = fv[k];
+      }
+      for (int e = lane + 64 * kFPer; e < fcnt; e += 64) Fw[e] = fsrc[e];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kFPer; ++k) {
+        const int e = lane + 64 * k;
+        if (e < fcnt) {
+          const int r = e / C, cc2 = e - r * C;
+          Fw[cc2 * frows + r] = fv[k];
+        }
+      }
+      for (int e = lane + 64 * kFPer; e < fcnt; e += 64) {
+        const int r = e / C, cc2 = e - r * C;
+        Fw[cc2 * frows + r] = fsrc[e];
+      }
+    }
+  }
+  const float* Fl = CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo;
+  const int fstep = CT > 0 ? C : 1;
+  const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
+  const int jt = tid / 3, q = tid - 3 * (tid / 3);
 
-    sfor<HI - LO>([&](auto Lc) {
-      constexpr int l = LO + LV_CV(Lc);
-      if (l < hi) {
+  for (int64_t g = blockIdx.x; g < a.groups; g += gridDim.x) {
+    const int64_t s0 = g * Sw;
+    const int Sv = (int)min((int64_t)Sw, a.n - s0);
+    const bool active = j < Sv;
+    const int nbytes = Sv * (int)MC * 4;
+    // 1. upstream-gradient tile: issue the 16-byte loads first
+    const float* gsrc = a.gout + s0 * MC;
+    const int mis = (int)(reinterpret_cast<uintptr_t>(gsrc) & 15);
+    char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
+    const int head = min((16 - mis) & 15, nbytes);
+    const int nvec = (nbytes - head) >> 4;
+    const int tail0 = head + nvec * 16;
+    const __amdgpu_buffer_rsrc_t rg =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gsrc), 0, nbytes, kRawBufferFlags);
+    f4 gv[kBwdLoadsPerThread];
+#pragma unroll
+    for (int k = 0; k < kBwdLoadsPerThread; ++k) {
+      const int v = tid + k * nthr;
+      if (v < nvec)
+        gv[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rg, head + 16 * v, 0, 0));
+    }
+    // 2. prologue task (sample jt, slot q): sincos, multiples of slot q
+    if (task) {
+      const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
+      float cc[3], ss[3], c1[3], s1[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) sincosf(a.ang[st * 3 + i], &ss[i], &cc[i]);
+      if (a.transpose) {
+        c1[0] = cc[2]; s1[0] = -ss[2];
+        c1[1] = cc[1]; s1[1] = -ss[1];
+        c1[2] = cc[0]; s1[2] = -ss[0];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { c1[i] = cc[i]; s1[i] = ss[i]; }
+      }
+      trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
+    }
+    // 3. tile into LDS: the loaded body, the rest, head/tail elements
+#pragma unroll
+    for (int k = 0; k < kBwdLoadsPerThread; ++k) {
+      const int v = tid + k * nthr;
+      if (v < nvec) *reinterpret_cast<f4*>(stage_b + head + 16 * v) = gv[k];
+    }
+    for (int v = tid + kBwdLoadsPerThread * nthr; v < nvec; v += nthr)
+      *reinterpret_cast<f4*>(stage_b + head + 16 * v) =
+          __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rg, head + 16 * v, 0, 0));
+    {
+      const int nedge = head / 4 + (nbytes - tail0) / 4;
+      if (tid < nedge) {
+        const int b = tid < head / 4 ? tid * 4 : tail0 + (tid - head / 4) * 4;
+        *reinterpret_cast<float*>(stage_b + b) =
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, b, 0, 0));
+      }
+    }
+    block_sync_lds();
+
+    float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
+    const float* tj = trig + min(j, Sw - 1) * kRow;
+    const float* Fs = a.F + (s0 + min(j, Sv - 1)) * a.Fstride + c;  // per-sample spectrum
+    float ga = 0.f, gb = 0.f, gc = 0.f;
+    sfor<LT + 1>([&](auto Lc) {
+      constexpr int l = LV_CV(Lc);
+      if (l >= lo && l < hi) {
         constexpr int nn = 2 * l + 1;
         constexpr int r0 = l * l;
-        const int rowlen = nn * C;
-        const int total = Sv * rowlen;
-        const int q64 = 64 / rowlen, r64 = 64 - q64 * rowlen;
-        // stage gout rows (contiguous) into LDS, then read columns
+        // live arrays kept to three or four of 2l+1: the spectrum column and G are
+        // re-read from LDS where they are needed again
+        float p2[nn], p4[nn], gq[nn], u[nn];
         {
-          int jj = lane / rowlen, w = lane - jj * rowlen;
-          const float* src0 = a.gout + s0 * a.MC + (int64_t)r0 * C;
-          for (int e = lane; e < total; e += 64) {
-            stage[e] = src0[jj * a.MC + w];
-            jj += q64;
-            w += r64;
-            if (w >= rowlen) { w -= rowlen; ++jj; }
-          }
+          float f0[nn];
+          sfor<nn>([&](auto K) {
+            constexpr int k = LV_CV(K);
+            f0[k] = SHAREDF ? Fl[(r0 + k) * fstep] : Fs[(r0 + k) * C];
+          });
+          xm<l>(mult_lds<l, 2, LT>(tj), f0, u);   // P1
         }
-        wave_lds_sync();
-        float f0[nn], p2[nn], p4[nn], gq[nn], u[nn];
-        const float* Fp = Fbase + r0 * C;
-        sfor<nn>([&](auto K) {
-          constexpr int k = LV_CV(K);
-          f0[k] = active ? Fp[k * C] : 0.f;
-          gq[k] = active ? stage[(j * nn + k) * C + c] : 0.f;
-        });
-        wave_lds_sync();
-        xrot<l, 2>(t, f0, u);
-        jmul<l>(u, p2);
-        xrot<l, 1>(t, p2, u);
-        jmul<l>(u, p4);
-        ga += xrot_dot_deriv<l, 0>(t, gq, p4);
-        xrot_t<l, 0>(t, gq, u);   // Q4
-        jmul<l>(u, p4);           // Q3 (reuse p4)
-        gb += xrot_dot_deriv<l, 1>(t, p4, p2);
-        xrot_t<l, 1>(t, p4, u);   // Q2
-        jmul<l>(u, p2);           // Q1 (reuse p2)
-        gc += xrot_dot_deriv<l, 2>(t, p2, f0);
-        xrot_t<l, 2>(t, p2, u);   // dF column
-        if (sharedF) {
-          // sum over the wave's samples: stage [j][i][c], then owners add in order
-          if (active) {
-            sfor<nn>([&](auto I) {
-              constexpr int i = LV_CV(I);
-              stage[(j * nn + i) * C + c] = u[i];
-            });
-          }
+        jmul<l>(u, p2);                           // P2
+        xm<l>(mult_lds<l, 1, LT>(tj), p2, u);     // P3
+        jmul<l>(u, p4);                           // P4
+        sfor<nn>([&](auto K) { gq[LV_CV(K)] = active ? tile_lane[(r0 + LV_CV(K)) * C] : 0.f; });
+        {
+          const Mult<l> ma = mult_lds<l, 0, LT>(tj);
+          ga += xm_dd<l>(ma, gq, p4);
+          xm_t<l>(ma, gq, u);                     // Q4
+        }
+        jmul<l>(u, p4);                           // Q3 (reuse p4)
+        {
+          const Mult<l> mb = mult_lds<l, 1, LT>(tj);
+          gb += xm_dd<l>(mb, p4, p2);
+          xm_t<l>(mb, p4, u);                     // Q2
+        }
+        jmul<l>(u, p2);                           // Q1 (reuse p2)
+        {
+          const Mult<l> mc = mult_lds<l, 2, LT>(tj);
+          float f0[nn];
+          sfor<nn>([&](auto K) {
+            constexpr int k = LV_CV(K);
+            f0[k] = SHAREDF ? Fl[(r0 + k) * fstep] : Fs[(r0 + k) * C];
+          });
+          gc += xm_dd<l>(mc, p2, f0);
+          xm_t<l>(mc, p2, u);                     // dF column
+        }
+        if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
+        if constexpr (SHAREDF) {
+          // this degree's rows summed over the group's samples in sample order, added to
+          // the block's slab (groups in order)
           wave_lds_sync();
-          float* acc = facc + (r0 - rows_lo) * C;
-          for (int e = lane; e < rowlen; e += 64) {
-            float sum = acc[e];
-            for (int jj = 0; jj < Sv; ++jj) sum += stage[jj * rowlen + e];
-            acc[e] = sum;
+          const float* col0 = reinterpret_cast<const float*>(stage_b) + r0 * C;
+          for (int e = lane; e < nn * C; e += 64) {
+            float sum = col0[e];
+            for (int jj = 1; jj < Sv; ++jj) sum += col0[jj * MC + e];
+            slabL[r0 * C + e] += sum;
           }
-          wave_lds_sync();
-        } else {
-          if (active) {
-            sfor<nn>([&](auto I) {
-              constexpr int i = LV_CV(I);
-              stage[(j * nn + i) * C + c] = u[i];
-            });
-          }
-          wave_lds_sync();
-          int jj = lane / rowlen, w = lane - jj * rowlen;
-          float* dst0 = a.gF + s0 * a.MC + (int64_t)r0 * C;
-          for (int e = lane; e < total; e += 64) {
-            dst0[jj * a.MC + w] = stage[e];
-            jj += q64;
-            w += r64;
-            if (w >= rowlen) { w -= rowlen; ++jj; }
-          }
-          wave_lds_sync();
         }
       }
     });
-    // angle partials: sum over the C lanes of each sample in column order
-    float g3[3];
-    if (a.transpose) { g3[0] = -gc; g3[1] = -gb; g3[2] = -ga; }
-    else { g3[0] = ga; g3[1] = gb; g3[2] = gc; }
-    apart[lane * 3 + 0] = g3[0];
-    apart[lane * 3 + 1] = g3[1];
-    apart[lane * 3 + 2] = g3[2];
-    wave_lds_sync();
-    if (active && c == 0) {
-      float r[3] = {0.f, 0.f, 0.f};
-      for (int cc2 = 0; cc2 < C; ++cc2)
-        for (int i = 0; i < 3; ++i) r[i] += apart[(lane + cc2) * 3 + i];
-      float* dst = a.ws_ang + ((int64_t)a.slot * a.n + s) * 3;
-      dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2];
+    // angle gradients: sum over the C lanes of a sample (column order), then segments
+    float* ap = apart + wave * 64 * 3;
+    if (a.transpose) {
+      ap[lane * 3 + 0] = -gc; ap[lane * 3 + 1] = -gb; ap[lane * 3 + 2] = -ga;
+    } else {
+      ap[lane * 3 + 0] = ga; ap[lane * 3 + 1] = gb; ap[lane * 3 + 2] = gc;
     }
-    wave_lds_sync();
+    block_sync_lds();
+    if (tid < 3 * Sv) {
+      const int js = tid / 3, i = tid - 3 * (tid / 3);
+      const int nw = nthr >> 6;
+      float r = 0.f;
+      for (int w = 0; w < nw; ++w) {
+        float sw = 0.f;
+        for (int cc2 = 0; cc2 < C; ++cc2) sw += apart[(w * 64 + js * C + cc2) * 3 + i];
+        r += sw;
+      }
+      a.gang[(s0 + js) * 3 + i] = r;
+    }
+    if constexpr (!SHAREDF)
+      tile_flush<float, 1>(a.gF + s0 * MC, stage_b, mis, nbytes, tid, nthr);
+    block_sync_lds();  // the next group overwrites the tile, the table and the partials
   }
-  if (sharedF) {
-    __syncthreads();
-    // block slab: sum the 4 wave accumulators in wave order
-    const float* acc0 = lds + 64 * (2 * LT + 1) + 64 * 3;
-    float* slab = a.ws_F + (int64_t)blockIdx.x * a.MC + (int64_t)rows_lo * C;
-    for (int e = threadIdx.x; e < seg_len; e += kThreads) {
-      float sum = 0.f;
-      for (int w = 0; w < kWavesPerBlock; ++w) sum += acc0[w * wave_floats + e];
-      slab[e] = sum;
-    }
+  if constexpr (SHAREDF) {
+    float* slab = a.ws_F + (int64_t)blockIdx.x * MC;
+    for (int e = lane; e < fcnt; e += 64) slab[rows_lo * C + e] = slabL[rows_lo * C + e];
   }
 }
 
+// Slab count per block of action_bwd_reduce_kernel (defined in action.hip).
+constexpr int kBwdReduceWaves = 16;
+
 struct BwdLaunch {
   ActionBwdArgs a;
-  int gx;
+  int gx, nseg;
+  size_t lds;
   hipStream_t stream;
 };
 
-template <int R>
+template <int LT>
 struct BwdLauncher {
-  static int run(BwdLaunch& p) {
-    const size_t lds = sizeof(float) * kWavesPerBlock *
-                       (size_t)bwd_wave_floats(R, p.a.L, p.a.C, p.a.Fstride == 0);
-    hipLaunchKernelGGL((action_bwd_kernel<R>), dim3(p.gx), dim3(kThreads), lds, p.stream, p.a);
-    LV_RETURN_LAUNCH("action_bwd_kernel");
-  }
+  static int run(BwdLaunch& p);  // out of class: see FwdLauncher
 };
+template <int LT>
+int BwdLauncher<LT>::run(BwdLaunch& p) {
+  const dim3 grid(p.gx), block(64 * p.nseg);
+  if (p.a.Fstride != 0)
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, false>), grid, block, p.lds, p.stream, p.a);
+  else if (p.a.C == kTileFastC)
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, true>), grid, block, p.lds, p.stream, p.a);
+  else
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, true>), grid, block, p.lds, p.stream, p.a);
+  LV_RETURN_LAUNCH("action_bwd_tile_kernel");
+}
 
-#define LV_EXTERN_BWD(R) extern template struct BwdLauncher<R>;
+#define LV_EXTERN_BWD(L) extern template struct BwdLauncher<L>;
 
 }  // namespace lv

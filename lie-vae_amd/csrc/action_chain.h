@@ -68,9 +68,9 @@ __device__ __forceinline__ void xrot(const TrigTab<LT>& t, const float (&x)[2 * 
   });
 }
 
-// The same multiples kept in LDS instead of registers (large l: the register table is
-// 6(l+1) VGPRs and caps occupancy at 2 waves per SIMD at l = 20).  Row of one sample:
-// [2A][f] = cos(f θ_A), [2A+1][f] = sin(f θ_A), f = 0..TP-1; kTrigRow floats per sample
+// The same multiples kept in LDS instead of registers (the register table is 6(l+1)
+// VGPRs).  Row of one sample: [2A][f] = cos(f θ_A), [2A+1][f] = sin(f θ_A),
+// f = 0..TP-1 (TP a multiple of 4: 16-byte aligned reads); kRow floats per sample
 // (padded so the samples of a wave fall in different LDS banks).
 template <int LT>
 struct TrigLds {
@@ -106,20 +106,36 @@ __device__ __forceinline__ void trig_row_fill(float* tj, const float c1[3], cons
   });
 }
 
-// y = X_l(θ_A) x with the multiples read from an LDS row (bitwise equal to xrot).
+// y = X_l(θ_A) x with the multiples read from an LDS row (bitwise equal to xrot): the
+// l+1 needed (cos, sin) pairs are fetched with 16-byte reads right before the product,
+// so they occupy registers only while it runs.
 template <int l, int A, int LT>
 __device__ __forceinline__ void xrot_lds(const float* tj, const float (&x)[2 * l + 1],
                                          float (&y)[2 * l + 1]) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int TP = TrigLds<LT>::TP;
+  float cc[l + 1], ss[l + 1];
+  sfor<(l + 4) / 4>([&](auto K) {
+    constexpr int k4 = LV_CV(K);
+    const f4 cv = *reinterpret_cast<const f4*>(tj + 2 * A * TP + 4 * k4);
+    const f4 sv = *reinterpret_cast<const f4*>(tj + (2 * A + 1) * TP + 4 * k4);
+    sfor<4>([&](auto I) {
+      constexpr int f = 4 * k4 + LV_CV(I);
+      if constexpr (f <= l) {
+        cc[f] = cv[LV_CV(I)];
+        ss[f] = sv[LV_CV(I)];
+      }
+    });
+  });
   sfor<2 * l + 1>([&](auto I) {
     constexpr int i = LV_CV(I);
     constexpr int f = l - i;
     if constexpr (f == 0) {
       y[i] = x[i];
     } else if constexpr (f > 0) {
-      y[i] = fmaf(tj[2 * A * TP + f], x[i], tj[(2 * A + 1) * TP + f] * x[2 * l - i]);
+      y[i] = fmaf(cc[f], x[i], ss[f] * x[2 * l - i]);
     } else {
-      y[i] = fmaf(tj[2 * A * TP - f], x[i], -(tj[(2 * A + 1) * TP - f] * x[2 * l - i]));
+      y[i] = fmaf(cc[-f], x[i], -(ss[-f] * x[2 * l - i]));
     }
   });
 }

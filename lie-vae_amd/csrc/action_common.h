@@ -5,37 +5,12 @@
 #include "action_chain.h"
 #include "so3_device.h"
 
-// Diagnostic timestamps (tools/kbench.hip builds with -DLV_STAMPS; never in the library).
-#ifndef LV_STORE_MODE
-#define LV_STORE_MODE 0
-#endif
-#ifndef LV_PROLOGUE_MODE
-#define LV_PROLOGUE_MODE 0
-#endif
-#ifndef LV_TILE_DIAG
-#define LV_TILE_DIAG 0
-#endif
-#ifdef LV_STAMPS
-__device__ unsigned long long* lv_stamp_buf;
-#define LV_STAMP(slot)                                                                  \
-  do {                                                                                  \
-    if ((threadIdx.x & 63) == 0) {                                                      \
-      const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                   \
-      const unsigned long long w_ = ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * \
-                                    (blockDim.x >> 6) + (threadIdx.x >> 6);             \
-      lv_stamp_buf[w_ * 8 + (slot)] = t_;                                               \
-    }                                                                                   \
-  } while (0)
-#else
-#define LV_STAMP(slot) do {} while (0)
-#endif
-
 namespace lv {
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = 64 * kWavesPerBlock;
 constexpr int kMaxSeg = 16;
-constexpr int kTrigLdsMinL = 13;  // action_fwd_kernel keeps the trig table in LDS from here
+constexpr int kTrigLdsMinL = 13;  // action_fwd_kernel keeps its trig table in LDS from here
 
 struct ActionArgs {
   const float* ang;     // (n,3) angles (non-fused)
@@ -210,11 +185,6 @@ struct LaneIn {
 template <bool FUSED>
 __device__ __forceinline__ void lane_load(const ActionArgs& a, int64_t s, LaneIn& in) {
   if constexpr (FUSED) {
-#if LV_PROLOGUE_MODE == 2  // diagnostic: no input load (synthetic v from the index)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) in.v[i] = 0.3f + 0.001f * (float)((s * 3 + i) & 1023);
-    return;
-#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) in.v[i] = a.v[s * 3 + i];
     if (a.mu) {
@@ -234,12 +204,6 @@ __device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& i
                                             bool active, int c, bool write_ang, float c1[3],
                                             float s1[3]) {
   float cc[3], ss[3];
-#if LV_PROLOGUE_MODE == 1  // diagnostic: trivial angles (loads kept)
-  if (true) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) { cc[i] = in.v[i]; ss[i] = in.v[(i + 1) % 3]; }
-  } else
-#endif
   if constexpr (FUSED) {
     float q[4];
     if (a.mu) {

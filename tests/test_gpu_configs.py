@@ -135,7 +135,21 @@ def test_config3_conv_vae_b512(gpu_device):
 
 def test_config3_dp_trainer_step_world1(gpu_device):
     """One data-parallel trainer step (world 1, reference loss, global-norm clip 1e-5,
-    Adam) on the config-3 model: finite, and the same twice from the same state."""
+    Adam) on the config-3 model: finite, and the same twice from the same state.  MIOpen
+    is pinned to deterministic algorithms for the comparison (its default backward-weight
+    convolutions may accumulate in any order); the SO(3) kernels are deterministic by
+    construction."""
+    from lie_vae.experiments.train_dp import DPTrainer
+    from lie_vae.experiments.vae import VAE
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        _dp_trainer_step_world1(gpu_device)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+
+
+def _dp_trainer_step_world1(gpu_device):
     from lie_vae.experiments.train_dp import DPTrainer
     from lie_vae.experiments.vae import VAE
     torch.manual_seed(0)

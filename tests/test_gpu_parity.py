@@ -287,6 +287,56 @@ def test_fused_matches_modular_and_grads(gpu_device):
         assert_normwise(host(a.grad)[None], host(b.grad)[None], 1e-4, what=f"grad {w}")
 
 
+def test_action_bwd_reproducible_and_looped(gpu_device):
+    """lv_group_action_bwd (backward tile kernel + dF slab reduce) is bitwise reproducible
+    (no atomics), agrees with the oracle's autograd, and its grid-capped path -- blocks
+    looping over several sample groups, n > 4096 groups -- gives the per-sample angle
+    gradients bit for bit and dF to fp32 summation-order noise."""
+    import lie_vae._ops as ops
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(11)
+    for L, n, transpose, shared in [(10, 4099, False, True), (10, 777, True, True),
+                                    (3, 1001, False, False), (12, 300, False, True)]:
+        ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n))
+        M = (L + 1) ** 2
+        F = torch.randn(M, 10, generator=gen) if shared else torch.randn(n, M, 10, generator=gen)
+        gout = torch.randn(n, M, 10, generator=gen)
+        grads = []
+        for _ in range(2):
+            a = ang.to(gpu_device).requires_grad_(True)
+            f = F.to(gpu_device).requires_grad_(True)
+            (ops.group_action(a, f, L, transpose=transpose) * gout.to(gpu_device)).sum().backward()
+            grads.append((host(a.grad), host(f.grad)))
+        assert np.array_equal(grads[0][0], grads[1][0]) and np.array_equal(grads[0][1], grads[1][1]), \
+            ("not reproducible", L, n, transpose, shared)
+        m = min(n, 300)
+        a64 = ang[:m].double().requires_grad_(True)
+        f64 = (F if shared else F[:m]).double().requires_grad_(True)
+        fe = f64.expand(m, -1, -1) if shared else f64
+        (lie_ref.block_wigner_apply(a64, fe, L, transpose=transpose) * gout[:m].double()).sum().backward()
+        assert_normwise(grads[0][0][:m], a64.grad.numpy(), 1e-4, what=f"gang L={L}")
+        if not shared:
+            assert_normwise(grads[0][1][:m].reshape(m, -1), f64.grad.numpy().reshape(m, -1), 1e-4,
+                            what=f"gF L={L}")
+    # looped path: 50,000 samples = 8,334 groups > the 4,096-block cap
+    L, n = 10, 50000
+    ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n)).to(gpu_device)
+    F = torch.randn((L + 1) ** 2, 10, generator=gen).to(gpu_device)
+    gout = torch.randn(n, (L + 1) ** 2, 10, generator=gen).to(gpu_device)
+    a = ang.clone().requires_grad_(True)
+    f = F.clone().requires_grad_(True)
+    (ops.group_action(a, f, L) * gout).sum().backward()
+    ga_parts, gf_sum = [], torch.zeros_like(F, dtype=torch.float64)
+    for lo in range(0, n, 4096):
+        ap = ang[lo:lo + 4096].clone().requires_grad_(True)
+        fp = F.clone().requires_grad_(True)
+        (ops.group_action(ap, fp, L) * gout[lo:lo + 4096]).sum().backward()
+        ga_parts.append(ap.grad)
+        gf_sum += fp.grad.double()
+    assert torch.equal(a.grad, torch.cat(ga_parts)), "angle gradients depend on the grid"
+    assert_normwise(host(f.grad)[None], gf_sum.cpu().numpy()[None], 1e-5, what="looped dF")
+
+
 def test_fused_vs_oracle_config2(gpu_device):
     """Config 2 exactly: B=4096, l=10, C=10, v ~ N(0,1), shared F (no mu)."""
     import lie_vae._ops as ops
@@ -366,43 +416,34 @@ def test_toy_dataset_generate(gpu_device):
                                rtol=1e-5)
 
 
-_PAIR_CHECK = r"""
-import sys, torch
-sys.path[:0] = [sys.argv[1], sys.argv[2]]
-import lie_vae._ops as ops
-import lie_vae.lie_tools as lt
-dev = torch.device("cuda:0")
-for L, n, transpose, bf16 in [(10, 4099, False, False), (10, 4096, True, False),
-                              (3, 1000, False, False), (12, 777, False, True)]:
-    gen = torch.Generator().manual_seed(7 + L + n)
-    v = torch.randn(n, 3, generator=gen).to(dev)
-    F11 = torch.randn((L + 1) ** 2, 11, generator=gen).to(dev)
-    F10 = F11[:, :10].contiguous()
-    od = torch.bfloat16 if bf16 else torch.float32
-    a = ops.fused_exp_action(None, v, F10, L, transpose=transpose, out_dtype=od)
-    b = ops.fused_exp_action(None, v, F11, L, transpose=transpose, out_dtype=od)
-    assert torch.equal(a, b[..., :10]), ("fused", L, n, transpose, bf16)
-    ang = lt.group_matrix_to_eazyz(lt.rodrigues(v))
-    a = ops.group_action(ang, F10, L, transpose=transpose, out_dtype=od)
-    b = ops.group_action(ang, F11, L, transpose=transpose, out_dtype=od)
-    assert torch.equal(a, b[..., :10]), ("angles", L, n, transpose, bf16)
-print("paired == scalar: ok")
-"""
-
-
-def test_paired_column_kernel_bitwise():
-    """The opt-in paired-column (packed fp32) tile kernel (LV_TILE_PAIR=1, C = 10) against
-    the scalar tile kernel (C = 11): columns are independent and both chains round
-    identically, so the first 10 columns must agree bit for bit (fused and angle inputs,
-    ragged last group, transpose, bf16 output).  The library reads the switch once per
-    process, hence the child process."""
-    import subprocess
-    import sys
-    from conftest import REPO
-    env = dict(os.environ, LV_TILE_PAIR="1")
-    r = subprocess.run([sys.executable, "-c", _PAIR_CHECK, os.path.join(REPO, "lie-vae_amd"), REPO],
-                       env=env, capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+def test_c10_specialised_tile_kernel_bitwise(gpu_device):
+    """The tile kernel is compiled twice: specialised for C = 10 (ActionNet's default
+    rep_copies; row-major spectrum staging, immediate offsets) and generic in C
+    (column-major staging).  Columns are independent and both chains round identically,
+    so C = 10 must agree bit for bit with the first 10 columns of C = 11 (fused and angle
+    inputs, ragged last group, transpose, bf16 output) -- and with the non-tile kernel
+    that a per-sample spectrum takes."""
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    DEV = gpu_device
+    for L, n, transpose, bf16 in [(10, 4099, False, False), (10, 4096, True, False),
+                                  (3, 1000, False, False), (12, 777, False, True),
+                                  (20, 301, False, False)]:
+        gen = torch.Generator().manual_seed(7 + L + n)
+        v = torch.randn(n, 3, generator=gen).to(DEV)
+        F11 = torch.randn((L + 1) ** 2, 11, generator=gen).to(DEV)
+        F10 = F11[:, :10].contiguous()
+        od = torch.bfloat16 if bf16 else torch.float32
+        a = ops.fused_exp_action(None, v, F10, L, transpose=transpose, out_dtype=od)
+        b = ops.fused_exp_action(None, v, F11, L, transpose=transpose, out_dtype=od)
+        assert torch.equal(a, b[..., :10]), ("fused", L, n, transpose, bf16)
+        ang = lt.group_matrix_to_eazyz(lt.rodrigues(v))
+        a = ops.group_action(ang, F10, L, transpose=transpose, out_dtype=od)
+        b = ops.group_action(ang, F11, L, transpose=transpose, out_dtype=od)
+        assert torch.equal(a, b[..., :10]), ("angles", L, n, transpose, bf16)
+        if not bf16:  # per-sample spectrum: the register-multiples, row-pair-store kernel
+            c = ops.group_action(ang, F10.expand(n, -1, -1).contiguous(), L, transpose=transpose)
+            assert torch.equal(a, c), ("per-sample", L, n, transpose)
 
 
 # ------------------------------------------------ end to end: VAE glue + IWAE (a11-a16, f3)
