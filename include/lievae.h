@@ -61,6 +61,13 @@ int lv_so3_sample_fwd(const float* mu, const float* v, float* z, int64_t ns, int
 int lv_so3_sample_bwd(const float* mu, const float* v, const float* gz, float* gmu, float* gv,
                       int64_t ns, int64_t B, void* stream);
 
+/* ---- backward of z = mu @ exp(v) -> group_matrix_to_eazyz(z) in one pass ----
+ * reparameterize.py:269-273 -> vae.py:182 (the fused path's prologue).  mu may be NULL
+ * (z = exp(v)); then gmu is not written.  gang (n,3) -> gv (n,3), gmu (n,3,3).
+ * Bitwise the same as lv_so3_exp_fwd / lv_mat_to_eazyz_bwd / lv_so3_exp_bwd in turn. */
+int lv_exp_eazyz_vjp(const float* mu, const float* v, const float* gang, float* gmu, float* gv,
+                     int64_t n, void* stream);
+
 /* ---- quaternions_to_group_matrix: lie_tools.py:183-192 (a3) ---------------- */
 int lv_quat_to_mat_fwd(const float* q, float* R, int64_t n, void* stream);
 int lv_quat_to_mat_bwd(const float* q, const float* gR, float* gq, int64_t n, void* stream);

@@ -241,8 +241,11 @@ constexpr auto kWigRun = launcher_table<WigLauncher, WigLaunch>(std::make_intege
 // loop over groups).
 constexpr size_t kBwdMaxLds = 96 * 1024;
 constexpr int64_t kBwdMaxBlocks = 4096;
-constexpr double kBwdSegCostSmall = 2.2 * 340.0;
-constexpr double kBwdSegCostLarge = 2.2 * 560.0;
+// Per-wave backward chain cost target: the backward kernel is register-heavy (~256 VGPRs,
+// 2 waves per SIMD), so few long waves beat many short ones -- measured at batch 4096,
+// l = 10 (profiles/r02_bwd_nseg_sweep.txt): 1 / 2 / 3 / 4 / 6 / 8 segments ran
+// 40.8 / 32.0 / 42.6 / 39.1 / 44.8 / 45.5 us per call.
+constexpr double kBwdSegCost = 2.2 * 1000.0;
 
 struct BwdPlan {
   int Sw, nseg, gx, fpitch;
@@ -259,8 +262,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   for (int l = 0; l <= L; ++l) total += degree_cost(l, true);
   for (int Sw = 64 / C; Sw >= 1; --Sw) {
     const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
-    const double target = groups < kTileManyGroups ? kBwdSegCostSmall : kBwdSegCostLarge;
-    int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
+    int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / kBwdSegCost)));
     if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
     nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
     if (3 * Sw > 64 * nseg || nseg > 8) continue;

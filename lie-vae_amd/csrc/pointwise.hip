@@ -100,6 +100,45 @@ __global__ void so3_sample_bwd_k(const float* mu, const float* v, const float* g
   }
 }
 
+// Backward of the fused path's prologue, z = mu @ exp(v) (mu optional) -> ZYZ angles, in
+// one pass per sample: the composition of so3_sample_fwd/so3_exp_fwd, mat_to_eazyz_bwd
+// and so3_sample_bwd/so3_exp_bwd above (same device functions, same operation order,
+// hence bitwise the same gradients) without the three launches and the (n,3,3)
+// round trips through memory.  reparameterize.py:269-273 + vae.py:182 (autograd in the
+// reference).
+__global__ void exp_eazyz_vjp_k(const float* mu, const float* v, const float* ga, float* gmu,
+                                float* gv, int64_t n) {
+  LV_FOR_EACH(i, n) {
+    float a[3], r[9], z[9], q[4], g[3], gq[4], gz[9], o[3];
+    ld(v + i * 3, a);
+    ld(ga + i * 3, g);
+    rodrigues_fwd(a, r);
+    float m[9];
+    if (mu) {
+      ld(mu + i * 9, m);
+      matmul3(m, r, z);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) z[k] = r[k];
+    }
+    mat_to_quat_fwd(z, q, nullptr);
+    quat_to_eazyz_bwd(q, g, gq);
+    mat_to_quat_bwd(z, gq, gz);
+    if (mu) {
+      float t[9], gr[9], acc[9];
+      matmul3_nt(gz, r, t);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[k] = 0.f + t[k];
+      st(gmu + i * 9, acc);
+      matmul3_tn(m, gz, gr);
+      rodrigues_bwd(a, gr, o);
+    } else {
+      rodrigues_bwd(a, gz, o);
+    }
+    st(gv + i * 3, o);
+  }
+}
+
 __global__ void quat_to_mat_fwd_k(const float* q, float* R, int64_t n) {
   LV_FOR_EACH(i, n) {
     float a[4], r[9];
@@ -480,6 +519,11 @@ int lv_so3_sample_bwd(const float* mu, const float* v, const float* gz, float* g
     return LV_OK;
   }
   LV_LAUNCH1(so3_sample_bwd_k, n, mu, v, gz, gmu, gv, ns, B);
+}
+int lv_exp_eazyz_vjp(const float* mu, const float* v, const float* gang, float* gmu, float* gv,
+                     int64_t n, void* stream) {
+  LV_PTRS(v && gang && gv && (!mu || gmu));
+  LV_LAUNCH1(exp_eazyz_vjp_k, n, mu, v, gang, gmu, gv, n);
 }
 int lv_quat_to_mat_fwd(const float* q, float* R, int64_t n, void* stream) {
   LV_PTRS(q && R);

@@ -241,7 +241,8 @@ def _contig(t):
 
 
 class _FusedExpAction(torch.autograd.Function):
-    """mu@exp(v) -> ZYZ -> block D·F in one launch; backward through the modular kernels."""
+    """mu@exp(v) -> ZYZ -> block D·F in one launch; backward = the group-action backward
+    (angle and spectrum gradients) + one fused exp -> ZYZ VJP kernel."""
 
     @staticmethod
     def forward(ctx, mu, v, spec, L, transpose, out_dtype):
@@ -271,20 +272,10 @@ class _FusedExpAction(torch.autograd.Function):
         ws = torch.empty(max(ws_bytes, 1), device=v.device, dtype=torch.uint8)
         call("lv_group_action_bwd", ptr(ang), ptr(spec), ctx.stride, ptr(gout), ptr(gang),
              ptr(gspec), n, L, C, int(ctx.transpose), ptr(ws), ws_bytes, stream())
-        z = _empty((n, 3, 3), v)
-        if ctx.has_mu:
-            call("lv_so3_sample_fwd", ptr(mu), ptr(v), ptr(z), 1, n, stream())
-        else:
-            call("lv_so3_exp_fwd", ptr(v), ptr(z), n, stream())
-        gz = torch.empty_like(z)
-        call("lv_mat_to_eazyz_bwd", ptr(z), ptr(gang), ptr(gz), n, stream())
         gv = torch.empty_like(v)
-        gmu = None
-        if ctx.has_mu:
-            gmu = torch.empty_like(mu)
-            call("lv_so3_sample_bwd", ptr(mu), ptr(v), ptr(gz), ptr(gmu), ptr(gv), 1, n, stream())
-        else:
-            call("lv_so3_exp_bwd", ptr(v), ptr(gz), ptr(gv), n, stream())
+        gmu = torch.empty_like(mu) if ctx.has_mu else None
+        call("lv_exp_eazyz_vjp", ptr(mu) if ctx.has_mu else None, ptr(v), ptr(gang), ptr(gmu),
+             ptr(gv), n, stream())
         return gmu, gv, gspec, None, None, None
 
 
