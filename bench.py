@@ -72,13 +72,6 @@ def algorithmic_bytes(batch, L, C, out_bytes):
     return batch * (12 + M * C * out_bytes) + M * C * 4
 
 
-def algorithmic_bytes_bwd(batch, L, C):
-    """Backward of the fused path: read angles (12 B) + the output gradient (M·C·4) and
-    write the angle gradient (12 B) per sample; read F and write dF once."""
-    M = (L + 1) ** 2
-    return batch * (12 + M * C * 4 + 12) + 2 * M * C * 4
-
-
 def cpu_threads():
     """Cores this process may use: its affinity set, capped by the box's CPU share
     (OMP_NUM_THREADS, set to the allotted share on the GPU box)."""
@@ -363,7 +356,9 @@ def main():
 
 def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     """Training direction at the metric size: the fused forward and the full backward
-    (group-action backward kernels + ZYZ and exp VJPs) through the autograd ops."""
+    (group-action backward kernel + dF reduce + exp -> ZYZ VJP) through the autograd ops,
+    (a) eager (host launch overhead included) and (b) the same forward + backward
+    captured once in a hipGraph and replayed (whole-step capture, static tensors)."""
     import lie_vae._ops as ops
     B, C = v.shape[0], F.shape[1]
     vg = v.clone().requires_grad_(True)
@@ -386,28 +381,36 @@ def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     t = e0.elapsed_time(e1) / 1e3 / iters
-    # backward kernels alone (same autograd graph, forward excluded)
-    out = ops.fused_exp_action(None, vg, Fg, L)
+    # (b) graph-captured forward + backward
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(stream)
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            step()
+    stream.wait_stream(side)
     torch.cuda.synchronize(dev)
-    tb = []
-    for _ in range(20):
+    g = torch.cuda.CUDAGraph()
+    vg.grad = None
+    Fg.grad = None
+    with torch.cuda.graph(g):
         out = ops.fused_exp_action(None, vg, Fg, L)
-        b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        b0.record(stream)
         out.backward(gout)
-        b1.record(stream)
-        tb.append((b0, b1))
+    g.replay()
     torch.cuda.synchronize(dev)
-    tbs = sorted(b0.elapsed_time(b1) / 1e3 for b0, b1 in tb)
-    tb_med = tbs[len(tbs) // 2]
-    bb = algorithmic_bytes_bwd(B, L, C)
+    reps = 500
+    e0.record(stream)
+    for _ in range(reps):
+        g.replay()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    tg = e0.elapsed_time(e1) / 1e3 / reps
     kern = bench_action_bwd_kernel(vg.detach(), F, gout, L, dev)
-    return {"value": B / t, "unit": "samples/s", "us_per_step": t * 1e6,
-            "bwd_us_median": tb_med * 1e6, "bwd_algorithmic_bytes": bb,
-            "bwd_achieved_GBs": bb / tb_med / 1e9, "bwd_frac": bb / tb_med / 1e9 / HBM_PEAK_GBS,
+    return {"value": B / tg, "unit": "samples/s", "us_per_step": tg * 1e6,
+            "launch": "graph (forward + backward captured once, replayed)",
+            "eager_us_per_step": t * 1e6, "eager_value": B / t,
             "action_bwd": kern,
-            "note": "eager autograd (host launch overhead included); backward = "
-                    "action-backward kernel + dF reduce + exp/ZYZ VJPs"}
+            "note": "one training-direction pass: fused forward, group-action backward "
+                    "kernel + deterministic dF reduce + fused exp/ZYZ VJP"}
 
 
 def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):

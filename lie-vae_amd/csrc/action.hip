@@ -147,12 +147,15 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
   if (3 * Sw > 64 * nseg || nseg > 8) return false;
   plan_segments(L, nseg, kTilePrologue, false, a.seg_lo);
+  // spectrum in LDS: C = kTileFastC -> the whole (M, C) once, row-major; other C ->
+  // per-wave column-major slices below kTileFGlobalMinL, global memory from there
   int fp = 0;
-  for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
+  if (a.C != kTileFastC && L < kTileFGlobalMinL)
+    for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
   a.fpitch = (fp + 3) & ~3;
+  const size_t fl = a.C == kTileFastC ? (size_t)a.MC : (size_t)nseg * a.fpitch;
   const size_t trig = (size_t)Sw * (6 * ((L + 1 + 3) & ~3) + 4);  // TrigLds<L>::kRow per sample
-  const size_t lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) +
-                     sizeof(float) * ((size_t)nseg * a.fpitch + trig);
+  const size_t lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) + sizeof(float) * (fl + trig);
   if (lds > kTileMaxLds || groups > 0x7fffffff) return false;
   a.Sw = Sw;
   a.write_through = (int64_t)a.n * a.MC * out_bytes <= kWriteThroughMaxBytes ? 1 : 0;
@@ -215,7 +218,9 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   if (Fstride == 0 && plan_tile(p, L, ob))
     return dispatch_L<FwdLauncher>(L, p);
   const double P = fused ? kPrologueFused : kPrologueFwd;
-  const int nseg = choose_nseg(n, p.a.Sw, L, P, false);
+  static const int kEnvFwdNseg = env_int("LV_FWD_NSEG", 0);  // A/B testing only
+  const int nseg = kEnvFwdNseg > 0 ? std::min(kEnvFwdNseg, std::min(L + 1, kMaxSeg))
+                                   : choose_nseg(n, p.a.Sw, L, P, false);
   plan_segments(L, nseg, P, false, p.a.seg_lo);
   const int64_t gx = (n + (int64_t)p.a.Sw * kWavesPerBlock - 1) / ((int64_t)p.a.Sw * kWavesPerBlock);
   LV_CHECK_ARG(gx <= 0x7fffffff, "batch too large");

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
   const int Sw = a.Sw;
   const int64_t MC = CT > 0 ? (int64_t)(LT + 1) * (LT + 1) * CT : a.MC;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
   const int tid = (int)threadIdx.x, nthr = (int)blockDim.x;
   const int j = lane / C;
   const int c = lane - j * C;

@@ -11,6 +11,7 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = 64 * kWavesPerBlock;
 constexpr int kMaxSeg = 16;
 constexpr int kTrigLdsMinL = 13;  // action_fwd_kernel keeps its trig table in LDS from here
+constexpr int kTileFGlobalMinL = 13;  // the tile kernel reads the spectrum from global from here
 
 struct ActionArgs {
   const float* ang;     // (n,3) angles (non-fused)

@@ -28,7 +28,7 @@ template <int LT, bool FUSED, bool SHARED, typename OutT>
 __global__ __launch_bounds__(kThreads) void action_fwd_kernel(ActionArgs a) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
   const int C = a.C, Sw = a.Sw;
   const int j = lane / C;
   const int c = lane - j * C;
@@ -249,15 +249,22 @@ __device__ __forceinline__ void tile_flush_rt(OutT* gout, const char* stage_b, i
 //   4. Outputs parked in the LDS tile; barrier; one contiguous flush.
 // CT: compile-time C (0 = run-time a.C).  With CT the spectrum slice is staged row-major
 // ([row][c], no index division, immediate-offset reads); without it column-major.
+// With CT the waves' row-major slices are contiguous: the block holds the whole spectrum
+// once (M*C floats, 17.6 KB at l = 20) and each wave stages and reads its own rows.  With
+// run-time C from l_max >= kTileFGlobalMinL the spectrum is read from global memory
+// instead (no global store precedes the flush, so these loads never wait behind stores);
+// that costs ~10 cycles of address processing per wave load instruction, which is why
+// the C = 10 path keeps it in LDS (l = 20 bf16: 18.5 -> 5 us of skeleton, tools/c5bench).
 template <int LT, int CT, bool FUSED, typename OutT>
 __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kRow = TrigLds<LT>::kRow;
+  constexpr bool FG = CT == 0 && LT >= kTileFGlobalMinL;  // spectrum from global, no LDS
   const int C = CT > 0 ? CT : a.C;
   const int Sw = CT > 0 ? 64 / CT : a.Sw;
   const int64_t MC = CT > 0 ? (int64_t)(LT + 1) * (LT + 1) * CT : a.MC;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
   const int j = lane / C;
   const int c = lane - j * C;
   const int lo = a.seg_lo[wave], hi = a.seg_lo[wave + 1];
@@ -268,7 +275,9 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   const bool active = j < Sv;
   const int stage_bytes = tile_stage_bytes(Sw, MC, (int)sizeof(OutT));
   float* trig = lds + (stage_bytes >> 2);
-  float* Fw = trig + Sw * kRow + wave * a.fpitch;
+  // spectrum in LDS: CT > 0 the whole (M, C) row-major (each wave fills its rows), else
+  // per-wave column-major slices of a.fpitch floats
+  float* Fw = trig + Sw * kRow + (CT > 0 ? rows_lo * C : wave * a.fpitch);
   // 1. prologue task (sample jt, slot q); the host guarantees 3*Sw <= blockDim.x
   const int tid = (int)threadIdx.x;
   const bool task = tid < 3 * Sw;
@@ -277,9 +286,9 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   LaneIn in;
   if (task) lane_load<FUSED>(a, st, in);
   // 2. this wave's spectrum slice: loads now, LDS writes after the prologue maths
-  constexpr int kFPer = 6;
+  constexpr int kFPer = FG ? 1 : 6;
   float fv[kFPer];
-  const int fcnt = (hi * hi - rows_lo) * C;
+  const int fcnt = FG ? 0 : (hi * hi - rows_lo) * C;
   const float* fsrc = a.F + rows_lo * C;
 #pragma unroll
   for (int k = 0; k < kFPer; ++k) {
@@ -291,7 +300,8 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
     lane_angles<FUSED>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
     trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
   }
-  if constexpr (CT > 0) {
+  if constexpr (FG) {
+  } else if constexpr (CT > 0) {
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
       const int e = lane + 64 * k;
@@ -319,8 +329,10 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
   OutT* st_lane = reinterpret_cast<OutT*>(stage_b) + j * MC + c;
   const float* tj = trig + min(j, Sw - 1) * kRow;
-  const float* Fl = CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo;
-  const int fstep = CT > 0 ? C : 1;  // LDS stride between consecutive rows of a column
+  // spectrum column: LDS slice, or global (FG)
+  const float* Fl = FG ? a.F + c : (CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo);
+  // (CT > 0: Fw + c - rows_lo*C is the start of the block's full row-major copy + c)
+  const int fstep = (FG || CT > 0) ? C : 1;  // stride between consecutive rows of a column
 
   sfor<LT + 1>([&](auto Lc) {
     constexpr int l = LV_CV(Lc);

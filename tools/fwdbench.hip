@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
     plan(nseg, 60.0, b.seg_lo);
     b.fpitch = fslice(b, nseg);
     b.write_through = wt;
-    const size_t lds = tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)nseg * b.fpitch + (size_t)b.Sw * TrigLds<L>::kRow);
+    const size_t lds = tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)b.MC + (size_t)b.Sw * TrigLds<L>::kRow);
     Kern k = action_fwd_tile_kernel<L, C, true, float>;
     if (keep) {
       hipLaunchKernelGGL(k, dim3(gx), dim3(64 * nseg), lds, 0, b);

@@ -5,7 +5,7 @@
 set -u
 cd "$(dirname "$0")/.."
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-OUT=gpurun_out/pmc_ic
+OUT=gpurun_out/pmc_ic${PMC_TAG:-}
 mkdir -p $OUT
 run() {  # dir, counters, cmd...
   local d=$1 grp=$2; shift 2
@@ -14,7 +14,7 @@ run() {  # dir, counters, cmd...
   echo "$d rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $d.log; exit $rc; fi
 }
-for L in 10 20; do
+for L in ${PMC_LS:-10 20}; do
   B=$([ $L = 10 ] && echo 4096 || echo 8192)
   mkdir -p $OUT/L$L
   run $OUT/L$L/a "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" python3 tools/prof_fused.py $B 30 $L 10
