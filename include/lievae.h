@@ -91,6 +91,32 @@ int lv_s2s1_fwd(const float* axis, const float* cs, float* R, int64_t n, void* s
 int lv_s2s1_bwd(const float* axis, const float* cs, const float* gR, float* gaxis, float* gcs,
                 int64_t n, void* stream);
 
+/* ---- fp64 twins of the per-sample maps ---------------------------------------
+ * The reference's maps follow their input dtype (lie_tools.py:28-38,61: v.new_tensor,
+ * eye(dtype=v.dtype)) and its self-tests run them in fp64 (lie_tools.py:271-291).
+ * Same contracts as the fp32 entry points above, double pointers. */
+int lv_so3_exp_fwd_f64(const double* v, double* R, int64_t n, void* stream);
+int lv_so3_exp_bwd_f64(const double* v, const double* gR, double* gv, int64_t n, void* stream);
+int lv_so3_sample_fwd_f64(const double* mu, const double* v, double* z, int64_t ns, int64_t B,
+                          void* stream);
+int lv_so3_sample_bwd_f64(const double* mu, const double* v, const double* gz, double* gmu,
+                          double* gv, int64_t ns, int64_t B, void* stream);
+int lv_exp_eazyz_vjp_f64(const double* mu, const double* v, const double* gang, double* gmu,
+                         double* gv, int64_t n, void* stream);
+int lv_quat_to_mat_fwd_f64(const double* q, double* R, int64_t n, void* stream);
+int lv_quat_to_mat_bwd_f64(const double* q, const double* gR, double* gq, int64_t n, void* stream);
+int lv_mat_to_quat_fwd_f64(const double* R, double* q, int64_t n, void* stream);
+int lv_mat_to_quat_bwd_f64(const double* R, const double* gq, double* gR, int64_t n, void* stream);
+int lv_quat_to_eazyz_fwd_f64(const double* q, double* ang, int64_t n, void* stream);
+int lv_quat_to_eazyz_bwd_f64(const double* q, const double* gang, double* gq, int64_t n,
+                             void* stream);
+int lv_mat_to_eazyz_fwd_f64(const double* R, double* ang, int64_t n, void* stream);
+int lv_mat_to_eazyz_bwd_f64(const double* R, const double* gang, double* gR, int64_t n,
+                            void* stream);
+int lv_s2s1_fwd_f64(const double* axis, const double* cs, double* R, int64_t n, void* stream);
+int lv_s2s1_bwd_f64(const double* axis, const double* cs, const double* gR, double* gaxis,
+                    double* gcs, int64_t n, void* stream);
+
 /* ---- s2s2_gram_schmidt, fp64: lie_tools.py:81-89 (S2S2Mean, reparameterize.py:184-197)
  * Crosses along the last axis (the reference's torch.cross without dim is
  * wrong at batch 3; documented deviation). */

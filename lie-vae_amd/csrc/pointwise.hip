@@ -34,28 +34,30 @@ inline dim3 grid_for(int64_t n) {
 #define LV_FOR_EACH(i, n) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
 
-template <int K>
-__device__ __forceinline__ void ld(const float* p, float (&x)[K]) {
+template <typename T, int K>
+__device__ __forceinline__ void ld(const T* p, T (&x)[K]) {
 #pragma unroll
   for (int i = 0; i < K; ++i) x[i] = p[i];
 }
-template <int K>
-__device__ __forceinline__ void st(float* p, const float (&x)[K]) {
+template <typename T, int K>
+__device__ __forceinline__ void st(T* p, const T (&x)[K]) {
 #pragma unroll
   for (int i = 0; i < K; ++i) p[i] = x[i];
 }
 
-__global__ void so3_exp_fwd_k(const float* v, float* R, int64_t n) {
+template <typename T>
+__global__ void so3_exp_fwd_k(const T* v, T* R, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[3], r[9];
+    T a[3], r[9];
     ld(v + i * 3, a);
     rodrigues_fwd(a, r);
     st(R + i * 9, r);
   }
 }
-__global__ void so3_exp_bwd_k(const float* v, const float* gR, float* gv, int64_t n) {
+template <typename T>
+__global__ void so3_exp_bwd_k(const T* v, const T* gR, T* gv, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[3], g[9], o[3];
+    T a[3], g[9], o[3];
     ld(v + i * 3, a);
     ld(gR + i * 9, g);
     rodrigues_bwd(a, g, o);
@@ -64,10 +66,11 @@ __global__ void so3_exp_bwd_k(const float* v, const float* gR, float* gv, int64_
 }
 
 // z[s,b] = mu[b] @ exp(v[s,b])
-__global__ void so3_sample_fwd_k(const float* mu, const float* v, float* z, int64_t ns, int64_t B) {
+template <typename T>
+__global__ void so3_sample_fwd_k(const T* mu, const T* v, T* z, int64_t ns, int64_t B) {
   LV_FOR_EACH(i, ns * B) {
     const int64_t b = i % B;
-    float a[3], r[9], m[9], o[9];
+    T a[3], r[9], m[9], o[9];
     ld(v + i * 3, a);
     ld(mu + b * 9, m);
     rodrigues_fwd(a, r);
@@ -76,16 +79,17 @@ __global__ void so3_sample_fwd_k(const float* mu, const float* v, float* z, int6
   }
 }
 // gv[s,b] via exp backward of mu^T gz; gmu[b] = sum_s gz R^T (fixed order)
-__global__ void so3_sample_bwd_k(const float* mu, const float* v, const float* gz, float* gmu,
-                                 float* gv, int64_t ns, int64_t B) {
+template <typename T>
+__global__ void so3_sample_bwd_k(const T* mu, const T* v, const T* gz, T* gmu,
+                                 T* gv, int64_t ns, int64_t B) {
   LV_FOR_EACH(b, B) {
-    float m[9], acc[9];
+    T m[9], acc[9];
     ld(mu + b * 9, m);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+    for (int k = 0; k < 9; ++k) acc[k] = T(0);
     for (int64_t s = 0; s < ns; ++s) {
       const int64_t i = s * B + b;
-      float a[3], r[9], g[9], gr[9], t[9], o[3];
+      T a[3], r[9], g[9], gr[9], t[9], o[3];
       ld(v + i * 3, a);
       ld(gz + i * 9, g);
       rodrigues_fwd(a, r);
@@ -106,14 +110,15 @@ __global__ void so3_sample_bwd_k(const float* mu, const float* v, const float* g
 // hence bitwise the same gradients) without the three launches and the (n,3,3)
 // round trips through memory.  reparameterize.py:269-273 + vae.py:182 (autograd in the
 // reference).
-__global__ void exp_eazyz_vjp_k(const float* mu, const float* v, const float* ga, float* gmu,
-                                float* gv, int64_t n) {
+template <typename T>
+__global__ void exp_eazyz_vjp_k(const T* mu, const T* v, const T* ga, T* gmu,
+                                T* gv, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[3], r[9], z[9], q[4], g[3], gq[4], gz[9], o[3];
+    T a[3], r[9], z[9], q[4], g[3], gq[4], gz[9], o[3];
     ld(v + i * 3, a);
     ld(ga + i * 3, g);
     rodrigues_fwd(a, r);
-    float m[9];
+    T m[9];
     if (mu) {
       ld(mu + i * 9, m);
       matmul3(m, r, z);
@@ -125,10 +130,10 @@ __global__ void exp_eazyz_vjp_k(const float* mu, const float* v, const float* ga
     quat_to_eazyz_bwd(q, g, gq);
     mat_to_quat_bwd(z, gq, gz);
     if (mu) {
-      float t[9], gr[9], acc[9];
+      T t[9], gr[9], acc[9];
       matmul3_nt(gz, r, t);
 #pragma unroll
-      for (int k = 0; k < 9; ++k) acc[k] = 0.f + t[k];
+      for (int k = 0; k < 9; ++k) acc[k] = T(0) + t[k];
       st(gmu + i * 9, acc);
       matmul3_tn(m, gz, gr);
       rodrigues_bwd(a, gr, o);
@@ -139,17 +144,19 @@ __global__ void exp_eazyz_vjp_k(const float* mu, const float* v, const float* ga
   }
 }
 
-__global__ void quat_to_mat_fwd_k(const float* q, float* R, int64_t n) {
+template <typename T>
+__global__ void quat_to_mat_fwd_k(const T* q, T* R, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[4], r[9];
+    T a[4], r[9];
     ld(q + i * 4, a);
     quat_to_mat_fwd(a, r);
     st(R + i * 9, r);
   }
 }
-__global__ void quat_to_mat_bwd_k(const float* q, const float* gR, float* gq, int64_t n) {
+template <typename T>
+__global__ void quat_to_mat_bwd_k(const T* q, const T* gR, T* gq, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[4], g[9], o[4];
+    T a[4], g[9], o[4];
     ld(q + i * 4, a);
     ld(gR + i * 9, g);
     quat_to_mat_bwd(a, g, o);
@@ -157,17 +164,19 @@ __global__ void quat_to_mat_bwd_k(const float* q, const float* gR, float* gq, in
   }
 }
 
-__global__ void mat_to_quat_fwd_k(const float* R, float* q, int64_t n) {
+template <typename T>
+__global__ void mat_to_quat_fwd_k(const T* R, T* q, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float r[9], o[4];
+    T r[9], o[4];
     ld(R + i * 9, r);
     mat_to_quat_fwd(r, o, nullptr);
     st(q + i * 4, o);
   }
 }
-__global__ void mat_to_quat_bwd_k(const float* R, const float* gq, float* gR, int64_t n) {
+template <typename T>
+__global__ void mat_to_quat_bwd_k(const T* R, const T* gq, T* gR, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float r[9], g[4], o[9];
+    T r[9], g[4], o[9];
     ld(R + i * 9, r);
     ld(gq + i * 4, g);
     mat_to_quat_bwd(r, g, o);
@@ -175,17 +184,19 @@ __global__ void mat_to_quat_bwd_k(const float* R, const float* gq, float* gR, in
   }
 }
 
-__global__ void quat_to_eazyz_fwd_k(const float* q, float* ang, int64_t n) {
+template <typename T>
+__global__ void quat_to_eazyz_fwd_k(const T* q, T* ang, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[4], o[3];
+    T a[4], o[3];
     ld(q + i * 4, a);
     quat_to_eazyz_fwd(a, o);
     st(ang + i * 3, o);
   }
 }
-__global__ void quat_to_eazyz_bwd_k(const float* q, const float* ga, float* gq, int64_t n) {
+template <typename T>
+__global__ void quat_to_eazyz_bwd_k(const T* q, const T* ga, T* gq, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[4], g[3], o[4];
+    T a[4], g[3], o[4];
     ld(q + i * 4, a);
     ld(ga + i * 3, g);
     quat_to_eazyz_bwd(a, g, o);
@@ -193,18 +204,20 @@ __global__ void quat_to_eazyz_bwd_k(const float* q, const float* ga, float* gq, 
   }
 }
 
-__global__ void mat_to_eazyz_fwd_k(const float* R, float* ang, int64_t n) {
+template <typename T>
+__global__ void mat_to_eazyz_fwd_k(const T* R, T* ang, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float r[9], q[4], o[3];
+    T r[9], q[4], o[3];
     ld(R + i * 9, r);
     mat_to_quat_fwd(r, q, nullptr);
     quat_to_eazyz_fwd(q, o);
     st(ang + i * 3, o);
   }
 }
-__global__ void mat_to_eazyz_bwd_k(const float* R, const float* ga, float* gR, int64_t n) {
+template <typename T>
+__global__ void mat_to_eazyz_bwd_k(const T* R, const T* ga, T* gR, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float r[9], q[4], g[3], gq[4], o[9];
+    T r[9], q[4], g[3], gq[4], o[9];
     ld(R + i * 9, r);
     ld(ga + i * 3, g);
     mat_to_quat_fwd(r, q, nullptr);
@@ -214,19 +227,21 @@ __global__ void mat_to_eazyz_bwd_k(const float* R, const float* ga, float* gR, i
   }
 }
 
-__global__ void s2s1_fwd_k(const float* ax, const float* cs, float* R, int64_t n) {
+template <typename T>
+__global__ void s2s1_fwd_k(const T* ax, const T* cs, T* R, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[3], c[2], r[9];
+    T a[3], c[2], r[9];
     ld(ax + i * 3, a);
     ld(cs + i * 2, c);
     s2s1_fwd(a, c, r);
     st(R + i * 9, r);
   }
 }
-__global__ void s2s1_bwd_k(const float* ax, const float* cs, const float* gR, float* gax,
-                           float* gcs, int64_t n) {
+template <typename T>
+__global__ void s2s1_bwd_k(const T* ax, const T* cs, const T* gR, T* gax,
+                           T* gcs, int64_t n) {
   LV_FOR_EACH(i, n) {
-    float a[3], c[2], g[9], oa[3], oc[2];
+    T a[3], c[2], g[9], oa[3], oc[2];
     ld(ax + i * 3, a);
     ld(cs + i * 2, c);
     ld(gR + i * 9, g);
@@ -497,17 +512,17 @@ int lv_max_degree(void) { return LV_MAX_DEGREE; }
 
 int lv_so3_exp_fwd(const float* v, float* R, int64_t n, void* stream) {
   LV_PTRS(v && R);
-  LV_LAUNCH1(so3_exp_fwd_k, n, v, R, n);
+  LV_LAUNCH1(so3_exp_fwd_k<float>, n, v, R, n);
 }
 int lv_so3_exp_bwd(const float* v, const float* gR, float* gv, int64_t n, void* stream) {
   LV_PTRS(v && gR && gv);
-  LV_LAUNCH1(so3_exp_bwd_k, n, v, gR, gv, n);
+  LV_LAUNCH1(so3_exp_bwd_k<float>, n, v, gR, gv, n);
 }
 int lv_so3_sample_fwd(const float* mu, const float* v, float* z, int64_t ns, int64_t B, void* stream) {
   const int64_t n = ns * B;
   LV_CHECK_ARG(ns >= 0 && B >= 0, "bad sizes");
   LV_PTRS(mu && v && z);
-  LV_LAUNCH1(so3_sample_fwd_k, n, mu, v, z, ns, B);
+  LV_LAUNCH1(so3_sample_fwd_k<float>, n, mu, v, z, ns, B);
 }
 int lv_so3_sample_bwd(const float* mu, const float* v, const float* gz, float* gmu, float* gv,
                       int64_t ns, int64_t B, void* stream) {
@@ -518,53 +533,127 @@ int lv_so3_sample_bwd(const float* mu, const float* v, const float* gz, float* g
     (void)hipMemsetAsync(gmu, 0, sizeof(float) * 9 * B, (hipStream_t)stream);
     return LV_OK;
   }
-  LV_LAUNCH1(so3_sample_bwd_k, n, mu, v, gz, gmu, gv, ns, B);
+  LV_LAUNCH1(so3_sample_bwd_k<float>, n, mu, v, gz, gmu, gv, ns, B);
 }
 int lv_exp_eazyz_vjp(const float* mu, const float* v, const float* gang, float* gmu, float* gv,
                      int64_t n, void* stream) {
   LV_PTRS(v && gang && gv && (!mu || gmu));
-  LV_LAUNCH1(exp_eazyz_vjp_k, n, mu, v, gang, gmu, gv, n);
+  LV_LAUNCH1(exp_eazyz_vjp_k<float>, n, mu, v, gang, gmu, gv, n);
 }
 int lv_quat_to_mat_fwd(const float* q, float* R, int64_t n, void* stream) {
   LV_PTRS(q && R);
-  LV_LAUNCH1(quat_to_mat_fwd_k, n, q, R, n);
+  LV_LAUNCH1(quat_to_mat_fwd_k<float>, n, q, R, n);
 }
 int lv_quat_to_mat_bwd(const float* q, const float* gR, float* gq, int64_t n, void* stream) {
   LV_PTRS(q && gR && gq);
-  LV_LAUNCH1(quat_to_mat_bwd_k, n, q, gR, gq, n);
+  LV_LAUNCH1(quat_to_mat_bwd_k<float>, n, q, gR, gq, n);
 }
 int lv_mat_to_quat_fwd(const float* R, float* q, int64_t n, void* stream) {
   LV_PTRS(R && q);
-  LV_LAUNCH1(mat_to_quat_fwd_k, n, R, q, n);
+  LV_LAUNCH1(mat_to_quat_fwd_k<float>, n, R, q, n);
 }
 int lv_mat_to_quat_bwd(const float* R, const float* gq, float* gR, int64_t n, void* stream) {
   LV_PTRS(R && gq && gR);
-  LV_LAUNCH1(mat_to_quat_bwd_k, n, R, gq, gR, n);
+  LV_LAUNCH1(mat_to_quat_bwd_k<float>, n, R, gq, gR, n);
 }
 int lv_quat_to_eazyz_fwd(const float* q, float* ang, int64_t n, void* stream) {
   LV_PTRS(q && ang);
-  LV_LAUNCH1(quat_to_eazyz_fwd_k, n, q, ang, n);
+  LV_LAUNCH1(quat_to_eazyz_fwd_k<float>, n, q, ang, n);
 }
 int lv_quat_to_eazyz_bwd(const float* q, const float* gang, float* gq, int64_t n, void* stream) {
   LV_PTRS(q && gang && gq);
-  LV_LAUNCH1(quat_to_eazyz_bwd_k, n, q, gang, gq, n);
+  LV_LAUNCH1(quat_to_eazyz_bwd_k<float>, n, q, gang, gq, n);
 }
 int lv_mat_to_eazyz_fwd(const float* R, float* ang, int64_t n, void* stream) {
   LV_PTRS(R && ang);
-  LV_LAUNCH1(mat_to_eazyz_fwd_k, n, R, ang, n);
+  LV_LAUNCH1(mat_to_eazyz_fwd_k<float>, n, R, ang, n);
 }
 int lv_mat_to_eazyz_bwd(const float* R, const float* gang, float* gR, int64_t n, void* stream) {
   LV_PTRS(R && gang && gR);
-  LV_LAUNCH1(mat_to_eazyz_bwd_k, n, R, gang, gR, n);
+  LV_LAUNCH1(mat_to_eazyz_bwd_k<float>, n, R, gang, gR, n);
 }
 int lv_s2s1_fwd(const float* axis, const float* cs, float* R, int64_t n, void* stream) {
   LV_PTRS(axis && cs && R);
-  LV_LAUNCH1(s2s1_fwd_k, n, axis, cs, R, n);
+  LV_LAUNCH1(s2s1_fwd_k<float>, n, axis, cs, R, n);
 }
 int lv_s2s1_bwd(const float* axis, const float* cs, const float* gR, float* gaxis, float* gcs,
                 int64_t n, void* stream) {
   LV_PTRS(axis && cs && gR && gaxis && gcs);
-  LV_LAUNCH1(s2s1_bwd_k, n, axis, cs, gR, gaxis, gcs, n);
+  LV_LAUNCH1(s2s1_bwd_k<float>, n, axis, cs, gR, gaxis, gcs, n);
+}
+// fp64 twins of the per-sample maps above: the reference's maps follow the input dtype
+// (lie_tools.py:28-38,61 -- new_tensor / eye(dtype=v.dtype)), and its own self-tests run
+// them in fp64 (lie_tools.py:271-291).  Same templates, T = double.
+int lv_so3_exp_fwd_f64(const double* v, double* R, int64_t n, void* stream) {
+  LV_PTRS(v && R);
+  LV_LAUNCH1(so3_exp_fwd_k<double>, n, v, R, n);
+}
+int lv_so3_exp_bwd_f64(const double* v, const double* gR, double* gv, int64_t n, void* stream) {
+  LV_PTRS(v && gR && gv);
+  LV_LAUNCH1(so3_exp_bwd_k<double>, n, v, gR, gv, n);
+}
+int lv_so3_sample_fwd_f64(const double* mu, const double* v, double* z, int64_t ns, int64_t B, void* stream) {
+  const int64_t n = ns * B;
+  LV_CHECK_ARG(ns >= 0 && B >= 0, "bad sizes");
+  LV_PTRS(mu && v && z);
+  LV_LAUNCH1(so3_sample_fwd_k<double>, n, mu, v, z, ns, B);
+}
+int lv_so3_sample_bwd_f64(const double* mu, const double* v, const double* gz, double* gmu, double* gv,
+                      int64_t ns, int64_t B, void* stream) {
+  const int64_t n = B;
+  LV_CHECK_ARG(ns >= 0 && B >= 0, "bad sizes");
+  LV_PTRS(mu && v && gz && gmu && gv);
+  if (ns == 0) {
+    (void)hipMemsetAsync(gmu, 0, sizeof(double) * 9 * B, (hipStream_t)stream);
+    return LV_OK;
+  }
+  LV_LAUNCH1(so3_sample_bwd_k<double>, n, mu, v, gz, gmu, gv, ns, B);
+}
+int lv_exp_eazyz_vjp_f64(const double* mu, const double* v, const double* gang, double* gmu, double* gv,
+                     int64_t n, void* stream) {
+  LV_PTRS(v && gang && gv && (!mu || gmu));
+  LV_LAUNCH1(exp_eazyz_vjp_k<double>, n, mu, v, gang, gmu, gv, n);
+}
+int lv_quat_to_mat_fwd_f64(const double* q, double* R, int64_t n, void* stream) {
+  LV_PTRS(q && R);
+  LV_LAUNCH1(quat_to_mat_fwd_k<double>, n, q, R, n);
+}
+int lv_quat_to_mat_bwd_f64(const double* q, const double* gR, double* gq, int64_t n, void* stream) {
+  LV_PTRS(q && gR && gq);
+  LV_LAUNCH1(quat_to_mat_bwd_k<double>, n, q, gR, gq, n);
+}
+int lv_mat_to_quat_fwd_f64(const double* R, double* q, int64_t n, void* stream) {
+  LV_PTRS(R && q);
+  LV_LAUNCH1(mat_to_quat_fwd_k<double>, n, R, q, n);
+}
+int lv_mat_to_quat_bwd_f64(const double* R, const double* gq, double* gR, int64_t n, void* stream) {
+  LV_PTRS(R && gq && gR);
+  LV_LAUNCH1(mat_to_quat_bwd_k<double>, n, R, gq, gR, n);
+}
+int lv_quat_to_eazyz_fwd_f64(const double* q, double* ang, int64_t n, void* stream) {
+  LV_PTRS(q && ang);
+  LV_LAUNCH1(quat_to_eazyz_fwd_k<double>, n, q, ang, n);
+}
+int lv_quat_to_eazyz_bwd_f64(const double* q, const double* gang, double* gq, int64_t n, void* stream) {
+  LV_PTRS(q && gang && gq);
+  LV_LAUNCH1(quat_to_eazyz_bwd_k<double>, n, q, gang, gq, n);
+}
+int lv_mat_to_eazyz_fwd_f64(const double* R, double* ang, int64_t n, void* stream) {
+  LV_PTRS(R && ang);
+  LV_LAUNCH1(mat_to_eazyz_fwd_k<double>, n, R, ang, n);
+}
+int lv_mat_to_eazyz_bwd_f64(const double* R, const double* gang, double* gR, int64_t n, void* stream) {
+  LV_PTRS(R && gang && gR);
+  LV_LAUNCH1(mat_to_eazyz_bwd_k<double>, n, R, gang, gR, n);
+}
+int lv_s2s1_fwd_f64(const double* axis, const double* cs, double* R, int64_t n, void* stream) {
+  LV_PTRS(axis && cs && R);
+  LV_LAUNCH1(s2s1_fwd_k<double>, n, axis, cs, R, n);
+}
+int lv_s2s1_bwd_f64(const double* axis, const double* cs, const double* gR, double* gaxis, double* gcs,
+                int64_t n, void* stream) {
+  LV_PTRS(axis && cs && gR && gaxis && gcs);
+  LV_LAUNCH1(s2s1_bwd_k<double>, n, axis, cs, gR, gaxis, gcs, n);
 }
 int lv_s2s2_fwd_f64(const double* v1, const double* v2, double* R, int64_t n, void* stream) {
   LV_PTRS(v1 && v2 && R);

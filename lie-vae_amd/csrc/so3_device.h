@@ -1,20 +1,31 @@
 // Per-sample SO(3) math, forward and hand-derived backward, in registers.
 //
 // Every function restates one reference op (file:line under the reference root) and
-// keeps its fp32 evaluation order (the library is built with -ffp-contract=off, so
-// nothing here is silently fused into an FMA).  Backward functions return the
-// gradient autograd would produce for the same composition of torch ops.
+// keeps its evaluation order (the library is built with -ffp-contract=off, so nothing
+// here is silently fused into an FMA).  Backward functions return the gradient autograd
+// would produce for the same composition of torch ops.  The maps are templates on the
+// scalar type T: the reference's maps follow their input dtype (v.new_tensor,
+// eye(dtype=v.dtype), lie_tools.py:28-38,61), so fp64 inputs get fp64 kernels; T = T
+// is the hot path and compiles to exactly the former fp32 code.
 #pragma once
 #include <hip/hip_runtime.h>
 
 namespace lv {
 
+// Scalar-type helpers: overloads so that one template body gives the fp32 code
+// (sincosf) for float and the fp64 code (sincos) for double.
+template <typename T>
+struct lv_nondeduced { using type = T; };
+__device__ __forceinline__ void lv_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ void lv_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+
 // ---------------------------------------------------------------- rodrigues
 // lie_tools.py:17-43 (hat) and :56-64 (rodrigues).  K = hat(u), K2 = K@K.
-__device__ __forceinline__ void hat_sq(const float u[3], float K[9], float K2[9]) {
-  K[0] = 0.f;   K[1] = -u[2]; K[2] = u[1];
-  K[3] = u[2];  K[4] = 0.f;   K[5] = -u[0];
-  K[6] = -u[1]; K[7] = u[0];  K[8] = 0.f;
+template <typename T>
+__device__ __forceinline__ void hat_sq(const T u[3], T K[9], T K2[9]) {
+  K[0] = T(0.);   K[1] = -u[2]; K[2] = u[1];
+  K[3] = u[2];  K[4] = T(0.);   K[5] = -u[0];
+  K[6] = -u[1]; K[7] = u[0];  K[8] = T(0.);
   // (K@K)_ij summed k = 0..2 exactly as the matmul does (zero products drop out).
   K2[0] = -u[2] * u[2] - u[1] * u[1];
   K2[1] = u[1] * u[0];
@@ -27,66 +38,72 @@ __device__ __forceinline__ void hat_sq(const float u[3], float K[9], float K2[9]
   K2[8] = -u[1] * u[1] - u[0] * u[0];
 }
 
-__device__ __forceinline__ float norm3(const float v[3]) {
-  return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+template <typename T>
+__device__ __forceinline__ T norm3(const T v[3]) {
+  return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
 }
 
-__device__ __forceinline__ void rodrigues_fwd(const float v[3], float R[9]) {
-  const float th = norm3(v);
-  const float u[3] = {v[0] / th, v[1] / th, v[2] / th};  // NaN at th == 0, like the reference
-  float K[9], K2[9];
+template <typename T>
+__device__ __forceinline__ void rodrigues_fwd(const T v[3], T R[9]) {
+  const T th = norm3(v);
+  const T u[3] = {v[0] / th, v[1] / th, v[2] / th};  // NaN at th == 0, like the reference
+  T K[9], K2[9];
   hat_sq(u, K, K2);
-  float s, c;
-  sincosf(th, &s, &c);
-  const float omc = 1.f - c;
+  T s, c;
+  lv_sincos(th, &s, &c);
+  const T omc = T(1.) - c;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    const float eye = (i == 0 || i == 4 || i == 8) ? 1.f : 0.f;
+    const T eye = (i == 0 || i == 4 || i == 8) ? T(1.) : T(0.);
     R[i] = (eye + s * K[i]) + omc * K2[i];
   }
 }
 
 // d/du of <g, s K(u) + w (u u^T - |u|^2 I)>
-__device__ __forceinline__ void hat_sq_vjp(const float u[3], const float g[9], float s, float w,
-                                           float gu[3]) {
-  const float tr = g[0] + g[4] + g[8];
-  float gsym_u[3];
+template <typename T>
+__device__ __forceinline__ void hat_sq_vjp(const T u[3], const T g[9], T s, T w,
+                                           T gu[3]) {
+  const T tr = g[0] + g[4] + g[8];
+  T gsym_u[3];
 #pragma unroll
   for (int m = 0; m < 3; ++m)
     gsym_u[m] = (g[m * 3 + 0] + g[0 * 3 + m]) * u[0] + (g[m * 3 + 1] + g[1 * 3 + m]) * u[1] +
                 (g[m * 3 + 2] + g[2 * 3 + m]) * u[2];
-  gu[0] = s * (g[7] - g[5]) + w * (gsym_u[0] - 2.f * tr * u[0]);
-  gu[1] = s * (g[2] - g[6]) + w * (gsym_u[1] - 2.f * tr * u[1]);
-  gu[2] = s * (g[3] - g[1]) + w * (gsym_u[2] - 2.f * tr * u[2]);
+  gu[0] = s * (g[7] - g[5]) + w * (gsym_u[0] - T(2.) * tr * u[0]);
+  gu[1] = s * (g[2] - g[6]) + w * (gsym_u[1] - T(2.) * tr * u[1]);
+  gu[2] = s * (g[3] - g[1]) + w * (gsym_u[2] - T(2.) * tr * u[2]);
 }
 
 // (theta, u = v/theta) -> v chain rule.
-__device__ __forceinline__ void polar_vjp(const float v[3], float th, const float gu[3], float gth,
-                                          float gv[3]) {
-  const float dot = gu[0] * v[0] + gu[1] * v[1] + gu[2] * v[2];
-  const float inv = 1.f / th;
-  const float inv3 = inv * inv * inv;
+template <typename T>
+__device__ __forceinline__ void polar_vjp(const T v[3], T th, const T gu[3], T gth,
+                                          T gv[3]) {
+  const T dot = gu[0] * v[0] + gu[1] * v[1] + gu[2] * v[2];
+  const T inv = T(1.) / th;
+  const T inv3 = inv * inv * inv;
 #pragma unroll
   for (int i = 0; i < 3; ++i) gv[i] = gu[i] * inv - dot * v[i] * inv3 + gth * v[i] * inv;
 }
 
-__device__ __forceinline__ void rodrigues_bwd(const float v[3], const float gR[9], float gv[3]) {
-  const float th = norm3(v);
-  const float u[3] = {v[0] / th, v[1] / th, v[2] / th};
-  float K[9], K2[9];
+template <typename T>
+__device__ __forceinline__ void rodrigues_bwd(const T v[3], const T gR[9], T gv[3]) {
+  const T th = norm3(v);
+  const T u[3] = {v[0] / th, v[1] / th, v[2] / th};
+  T K[9], K2[9];
   hat_sq(u, K, K2);
-  float s, c;
-  sincosf(th, &s, &c);
-  float gth = 0.f;
+  T s, c;
+  lv_sincos(th, &s, &c);
+  T gth = T(0.);
 #pragma unroll
   for (int i = 0; i < 9; ++i) gth += gR[i] * (c * K[i] + s * K2[i]);
-  float gu[3];
-  hat_sq_vjp(u, gR, s, 1.f - c, gu);
+  T gu[3];
+  hat_sq_vjp(u, gR, s, T(1.) - c, gu);
   polar_vjp(v, th, gu, gth, gv);
 }
 
 // ------------------------------------------------------------------ 3x3 ops
-__device__ __forceinline__ void matmul3(const float A[9], const float B[9], float C[9]) {
+template <typename T>
+__device__ __forceinline__ void matmul3(const T A[9], const T B[9], T C[9]) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -95,7 +112,8 @@ __device__ __forceinline__ void matmul3(const float A[9], const float B[9], floa
                      A[i * 3 + 2] * B[2 * 3 + j];
 }
 // C = A^T B
-__device__ __forceinline__ void matmul3_tn(const float A[9], const float B[9], float C[9]) {
+template <typename T>
+__device__ __forceinline__ void matmul3_tn(const T A[9], const T B[9], T C[9]) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -104,7 +122,8 @@ __device__ __forceinline__ void matmul3_tn(const float A[9], const float B[9], f
                      A[2 * 3 + i] * B[2 * 3 + j];
 }
 // C = A B^T
-__device__ __forceinline__ void matmul3_nt(const float A[9], const float B[9], float C[9]) {
+template <typename T>
+__device__ __forceinline__ void matmul3_nt(const T A[9], const T B[9], T C[9]) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -115,27 +134,30 @@ __device__ __forceinline__ void matmul3_nt(const float A[9], const float B[9], f
 
 // ----------------------------------------------- group_matrix_to_quaternions
 // lie_tools.py:112-157: 4-case trace method, eps 1e-6, case = first argmax.
+template <typename T>
 struct QuatCase {
-  float pre[4];
-  float den[4];
+  T pre[4];
+  T den[4];
   int k;
 };
 
-__device__ __forceinline__ void mat_to_quat_fwd(const float r[9], float q[4], QuatCase* qc) {
-  const float a = r[0], b = r[4], c = r[8];
-  float pre[4] = {((1.f + a) - b) - c, ((1.f - a) + b) - c, ((1.f - a) - b) + c,
-                  ((1.f + a) + b) + c};
-  float den[4];
+template <typename T>
+__device__ __forceinline__ void mat_to_quat_fwd(const T r[9], T q[4],
+                                                typename lv_nondeduced<QuatCase<T>>::type* qc) {
+  const T a = r[0], b = r[4], c = r[8];
+  T pre[4] = {((T(1.) + a) - b) - c, ((T(1.) - a) + b) - c, ((T(1.) - a) - b) + c,
+                  ((T(1.) + a) + b) + c};
+  T den[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) den[i] = 0.5f * sqrtf(1e-6f + fabsf(pre[i]));
+  for (int i = 0; i < 4; ++i) den[i] = T(0.5) * sqrt(T(1e-6) + fabs(pre[i]));
   int k = 0;
-  float best = den[0];
+  T best = den[0];
 #pragma unroll
   for (int i = 1; i < 4; ++i)
     if (den[i] > best) { best = den[i]; k = i; }
-  const float s01 = r[1] + r[3], s02 = r[2] + r[6], s12 = r[5] + r[7];
-  const float d12 = r[5] - r[7], d20 = r[6] - r[2], d01 = r[1] - r[3];
-  const float d4 = 4.f * best;
+  const T s01 = r[1] + r[3], s02 = r[2] + r[6], s12 = r[5] + r[7];
+  const T d12 = r[5] - r[7], d20 = r[6] - r[2], d01 = r[1] - r[3];
+  const T d4 = T(4.) * best;
   switch (k) {
     case 0: q[0] = best;      q[1] = s01 / d4;  q[2] = s02 / d4;  q[3] = d12 / d4; break;
     case 1: q[0] = s01 / d4;  q[1] = best;      q[2] = s12 / d4;  q[3] = d20 / d4; break;
@@ -149,22 +171,23 @@ __device__ __forceinline__ void mat_to_quat_fwd(const float r[9], float q[4], Qu
   }
 }
 
-__device__ __forceinline__ void mat_to_quat_bwd(const float r[9], const float gq[4], float gr[9]) {
-  float q[4];
-  QuatCase qc;
+template <typename T>
+__device__ __forceinline__ void mat_to_quat_bwd(const T r[9], const T gq[4], T gr[9]) {
+  T q[4];
+  QuatCase<T> qc;
   mat_to_quat_fwd(r, q, &qc);
   const int k = qc.k;
-  const float d = qc.den[k];
-  const float inv4d = 1.f / (4.f * d);
+  const T d = qc.den[k];
+  const T inv4d = T(1.) / (T(4.) * d);
 #pragma unroll
-  for (int i = 0; i < 9; ++i) gr[i] = 0.f;
+  for (int i = 0; i < 9; ++i) gr[i] = T(0.);
   // gradient into the denominator: q_k = d, q_j = N_j / (4 d)
-  float gd = gq[k];
+  T gd = gq[k];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (j != k) gd -= gq[j] * q[j] / d;
   // N_j partials: index pairs (p, m, sign of second) for s01, s02, s12, d12, d20, d01
-  auto addN = [&](int which, float g) {
+  auto addN = [&](int which, T g) {
     switch (which) {
       case 0: gr[1] += g; gr[3] += g; break;   // s01
       case 1: gr[2] += g; gr[6] += g; break;   // s02
@@ -181,11 +204,11 @@ __device__ __forceinline__ void mat_to_quat_bwd(const float r[9], const float gq
   for (int j = 0; j < 4; ++j)
     if (j != k) addN(tab[k][j], gq[j] * inv4d);
   // d = 0.5 sqrt(1e-6 + |pre_k|)
-  const float t = sqrtf(1e-6f + fabsf(qc.pre[k]));
-  const float p = qc.pre[k];
-  const float sg = (p > 0.f) ? 1.f : ((p < 0.f) ? -1.f : 0.f);
-  const float gpre = gd * 0.25f / t * sg;
-  const float coef[4][3] = {{1.f, -1.f, -1.f}, {-1.f, 1.f, -1.f}, {-1.f, -1.f, 1.f}, {1.f, 1.f, 1.f}};
+  const T t = sqrt(T(1e-6) + fabs(qc.pre[k]));
+  const T p = qc.pre[k];
+  const T sg = (p > T(0.)) ? T(1.) : ((p < T(0.)) ? -T(1.) : T(0.));
+  const T gpre = gd * T(0.25) / t * sg;
+  const T coef[4][3] = {{T(1.), -T(1.), -T(1.)}, {-T(1.), T(1.), -T(1.)}, {-T(1.), -T(1.), T(1.)}, {T(1.), T(1.), T(1.)}};
   gr[0] += gpre * coef[k][0];
   gr[4] += gpre * coef[k][1];
   gr[8] += gpre * coef[k][2];
@@ -195,61 +218,69 @@ __device__ __forceinline__ void mat_to_quat_bwd(const float r[9], const float gq
 // lie_tools.py:160-175 (q scalar-last; beta clamped to [-1+1e-6, 1-1e-6]).
 constexpr float kEazyzLo = (float)(-1.0 + 1e-6);
 constexpr float kEazyzHi = (float)(1.0 - 1e-6);
+template <typename T>
+__device__ __forceinline__ T eazyz_lo() { return (T)(-1.0 + 1e-6); }
+template <typename T>
+__device__ __forceinline__ T eazyz_hi() { return (T)(1.0 - 1e-6); }
 
-__device__ __forceinline__ void quat_to_eazyz_fwd(const float q[4], float ang[3]) {
-  const float a1 = q[1] * q[2] - q[0] * q[3];
-  const float b1 = q[0] * q[2] + q[1] * q[3];
-  const float cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
-  const float a3 = q[0] * q[3] + q[1] * q[2];
-  const float b3 = q[1] * q[3] - q[0] * q[2];
-  ang[0] = atan2f(a1, b1);
-  ang[1] = acosf(fminf(fmaxf(cb, kEazyzLo), kEazyzHi));
-  ang[2] = atan2f(a3, b3);
+template <typename T>
+__device__ __forceinline__ void quat_to_eazyz_fwd(const T q[4], T ang[3]) {
+  const T a1 = q[1] * q[2] - q[0] * q[3];
+  const T b1 = q[0] * q[2] + q[1] * q[3];
+  const T cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
+  const T a3 = q[0] * q[3] + q[1] * q[2];
+  const T b3 = q[1] * q[3] - q[0] * q[2];
+  ang[0] = atan2(a1, b1);
+  ang[1] = acos(fmin(fmax(cb, eazyz_lo<T>()), eazyz_hi<T>()));
+  ang[2] = atan2(a3, b3);
 }
 
-__device__ __forceinline__ void quat_to_eazyz_bwd(const float q[4], const float ga[3], float gq[4]) {
-  const float a1 = q[1] * q[2] - q[0] * q[3];
-  const float b1 = q[0] * q[2] + q[1] * q[3];
-  const float cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
-  const float a3 = q[0] * q[3] + q[1] * q[2];
-  const float b3 = q[1] * q[3] - q[0] * q[2];
-  const float r1 = a1 * a1 + b1 * b1, r3 = a3 * a3 + b3 * b3;
-  const float ga1 = ga[0] * b1 / r1, gb1 = ga[0] * -a1 / r1;
-  const float ga3 = ga[2] * b3 / r3, gb3 = ga[2] * -a3 / r3;
-  const float x = fminf(fmaxf(cb, kEazyzLo), kEazyzHi);
-  const bool pass = (cb >= kEazyzLo) && (cb <= kEazyzHi);
-  const float gcb = pass ? (-ga[1] / sqrtf(1.f - x * x)) : 0.f;
-  gq[0] = -q[3] * ga1 + q[2] * gb1 + q[3] * ga3 - q[2] * gb3 - 2.f * q[0] * gcb;
-  gq[1] = q[2] * ga1 + q[3] * gb1 + q[2] * ga3 + q[3] * gb3 - 2.f * q[1] * gcb;
-  gq[2] = q[1] * ga1 + q[0] * gb1 + q[1] * ga3 - q[0] * gb3 + 2.f * q[2] * gcb;
-  gq[3] = -q[0] * ga1 + q[1] * gb1 + q[0] * ga3 + q[1] * gb3 + 2.f * q[3] * gcb;
+template <typename T>
+__device__ __forceinline__ void quat_to_eazyz_bwd(const T q[4], const T ga[3], T gq[4]) {
+  const T a1 = q[1] * q[2] - q[0] * q[3];
+  const T b1 = q[0] * q[2] + q[1] * q[3];
+  const T cb = ((q[3] * q[3] - q[0] * q[0]) - q[1] * q[1]) + q[2] * q[2];
+  const T a3 = q[0] * q[3] + q[1] * q[2];
+  const T b3 = q[1] * q[3] - q[0] * q[2];
+  const T r1 = a1 * a1 + b1 * b1, r3 = a3 * a3 + b3 * b3;
+  const T ga1 = ga[0] * b1 / r1, gb1 = ga[0] * -a1 / r1;
+  const T ga3 = ga[2] * b3 / r3, gb3 = ga[2] * -a3 / r3;
+  const T x = fmin(fmax(cb, eazyz_lo<T>()), eazyz_hi<T>());
+  const bool pass = (cb >= eazyz_lo<T>()) && (cb <= eazyz_hi<T>());
+  const T gcb = pass ? (-ga[1] / sqrt(T(1.) - x * x)) : T(0.);
+  gq[0] = -q[3] * ga1 + q[2] * gb1 + q[3] * ga3 - q[2] * gb3 - T(2.) * q[0] * gcb;
+  gq[1] = q[2] * ga1 + q[3] * gb1 + q[2] * ga3 + q[3] * gb3 - T(2.) * q[1] * gcb;
+  gq[2] = q[1] * ga1 + q[0] * gb1 + q[1] * ga3 - q[0] * gb3 + T(2.) * q[2] * gcb;
+  gq[3] = -q[0] * ga1 + q[1] * gb1 + q[0] * ga3 + q[1] * gb3 + T(2.) * q[3] * gcb;
 }
 
 // ------------------------------------------------ quaternions_to_group_matrix
 // lie_tools.py:183-192: normalise, then the reference's (transposed-active) matrix.
-__device__ __forceinline__ void quat_to_mat_fwd(const float q0[4], float R[9]) {
-  const float nrm = sqrtf(q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3]);
-  const float x = q0[0] / nrm, y = q0[1] / nrm, z = q0[2] / nrm, w = q0[3] / nrm;
+template <typename T>
+__device__ __forceinline__ void quat_to_mat_fwd(const T q0[4], T R[9]) {
+  const T nrm = sqrt(q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3]);
+  const T x = q0[0] / nrm, y = q0[1] / nrm, z = q0[2] / nrm, w = q0[3] / nrm;
   R[0] = ((x * x - y * y) - z * z) + w * w;
-  R[1] = 2.f * (x * y + z * w);
-  R[2] = 2.f * (x * z - y * w);
-  R[3] = 2.f * (x * y - z * w);
+  R[1] = T(2.) * (x * y + z * w);
+  R[2] = T(2.) * (x * z - y * w);
+  R[3] = T(2.) * (x * y - z * w);
   R[4] = ((-x * x + y * y) - z * z) + w * w;
-  R[5] = 2.f * (y * z + x * w);
-  R[6] = 2.f * (x * z + y * w);
-  R[7] = 2.f * (y * z - x * w);
+  R[5] = T(2.) * (y * z + x * w);
+  R[6] = T(2.) * (x * z + y * w);
+  R[7] = T(2.) * (y * z - x * w);
   R[8] = ((-x * x - y * y) + z * z) + w * w;
 }
 
-__device__ __forceinline__ void quat_to_mat_bwd(const float q0[4], const float g[9], float gq[4]) {
-  const float nrm = sqrtf(q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3]);
-  const float x = q0[0] / nrm, y = q0[1] / nrm, z = q0[2] / nrm, w = q0[3] / nrm;
-  float gn[4];
-  gn[0] = 2.f * (x * (g[0] - g[4] - g[8]) + y * (g[1] + g[3]) + z * (g[2] + g[6]) + w * (g[5] - g[7]));
-  gn[1] = 2.f * (-y * (g[0] - g[4] + g[8]) + x * (g[1] + g[3]) - w * (g[2] - g[6]) + z * (g[5] + g[7]));
-  gn[2] = 2.f * (-z * (g[0] + g[4] - g[8]) + w * (g[1] - g[3]) + x * (g[2] + g[6]) + y * (g[5] + g[7]));
-  gn[3] = 2.f * (w * (g[0] + g[4] + g[8]) + z * (g[1] - g[3]) - y * (g[2] - g[6]) + x * (g[5] - g[7]));
-  const float dot = gn[0] * x + gn[1] * y + gn[2] * z + gn[3] * w;
+template <typename T>
+__device__ __forceinline__ void quat_to_mat_bwd(const T q0[4], const T g[9], T gq[4]) {
+  const T nrm = sqrt(q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3]);
+  const T x = q0[0] / nrm, y = q0[1] / nrm, z = q0[2] / nrm, w = q0[3] / nrm;
+  T gn[4];
+  gn[0] = T(2.) * (x * (g[0] - g[4] - g[8]) + y * (g[1] + g[3]) + z * (g[2] + g[6]) + w * (g[5] - g[7]));
+  gn[1] = T(2.) * (-y * (g[0] - g[4] + g[8]) + x * (g[1] + g[3]) - w * (g[2] - g[6]) + z * (g[5] + g[7]));
+  gn[2] = T(2.) * (-z * (g[0] + g[4] - g[8]) + w * (g[1] - g[3]) + x * (g[2] + g[6]) + y * (g[5] + g[7]));
+  gn[3] = T(2.) * (w * (g[0] + g[4] + g[8]) + z * (g[1] - g[3]) - y * (g[2] - g[6]) + x * (g[5] - g[7]));
+  const T dot = gn[0] * x + gn[1] * y + gn[2] * z + gn[3] * w;
   gq[0] = (gn[0] - dot * x) / nrm;
   gq[1] = (gn[1] - dot * y) / nrm;
   gq[2] = (gn[2] - dot * z) / nrm;
@@ -258,25 +289,27 @@ __device__ __forceinline__ void quat_to_mat_bwd(const float q0[4], const float g
 
 // ------------------------------------------------------------- s2s1rodrigues
 // lie_tools.py:67-78: R = I + sin K + (1 - cos) K@K, K = hat(axis), (cos, sin) given.
-__device__ __forceinline__ void s2s1_fwd(const float a[3], const float cs[2], float R[9]) {
-  float K[9], K2[9];
+template <typename T>
+__device__ __forceinline__ void s2s1_fwd(const T a[3], const T cs[2], T R[9]) {
+  T K[9], K2[9];
   hat_sq(a, K, K2);
-  const float omc = 1.f - cs[0];
+  const T omc = T(1.) - cs[0];
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    const float eye = (i == 0 || i == 4 || i == 8) ? 1.f : 0.f;
+    const T eye = (i == 0 || i == 4 || i == 8) ? T(1.) : T(0.);
     R[i] = (eye + cs[1] * K[i]) + omc * K2[i];
   }
 }
 
-__device__ __forceinline__ void s2s1_bwd(const float a[3], const float cs[2], const float g[9],
-                                         float ga[3], float gcs[2]) {
-  float K[9], K2[9];
+template <typename T>
+__device__ __forceinline__ void s2s1_bwd(const T a[3], const T cs[2], const T g[9],
+                                         T ga[3], T gcs[2]) {
+  T K[9], K2[9];
   hat_sq(a, K, K2);
-  float gs = 0.f, gc = 0.f;
+  T gs = T(0.), gc = T(0.);
 #pragma unroll
   for (int i = 0; i < 9; ++i) { gs += g[i] * K[i]; gc -= g[i] * K2[i]; }
-  hat_sq_vjp(a, g, cs[1], 1.f - cs[0], ga);
+  hat_sq_vjp(a, g, cs[1], T(1.) - cs[0], ga);
   gcs[0] = gc;
   gcs[1] = gs;
 }

@@ -54,6 +54,13 @@ _SIGS = {
     "lv_so3_log_posterior_fwd": [_P, _P, _P, _I64, _I64, _I, _P],
     "lv_so3_log_posterior_bwd": [_P, _P, _P, _P, _P, _I64, _I64, _I, _P],
 }
+# fp64 twins of the per-sample maps (same argument lists, double pointers)
+for _name in ("lv_so3_exp_fwd", "lv_so3_exp_bwd", "lv_so3_sample_fwd", "lv_so3_sample_bwd",
+              "lv_exp_eazyz_vjp", "lv_quat_to_mat_fwd", "lv_quat_to_mat_bwd",
+              "lv_mat_to_quat_fwd", "lv_mat_to_quat_bwd", "lv_quat_to_eazyz_fwd",
+              "lv_quat_to_eazyz_bwd", "lv_mat_to_eazyz_fwd", "lv_mat_to_eazyz_bwd",
+              "lv_s2s1_fwd", "lv_s2s1_bwd"):
+    _SIGS[_name + "_f64"] = _SIGS[_name]
 _RESTYPES = {"lv_group_action_bwd_workspace": _SZ, "lv_last_error": ctypes.c_char_p}
 _SIGS_EXTRA = {"lv_group_action_bwd_workspace": [_I64, _I, _I, _I], "lv_last_error": []}
 

@@ -1,7 +1,9 @@
 """torch.autograd.Functions over the C ABI.  Forward and backward both run the HIP
 kernels of liblievae_hip.so on the caller's current stream; nothing here computes on
-the CPU.  Inputs are made contiguous fp32 (fp64 for the S2S2 Gram–Schmidt, as in the
-reference, ``reparameterize.py:195-197``)."""
+the CPU.  The per-sample maps follow the input dtype as the reference's do (fp64 in ->
+the ``*_f64`` kernels, fp64 out; anything else -> fp32); the Wigner-D / group-action
+path is fp32 (the reference's own J is fp32, ``lie_tools.py:10-14``) and the S2S2
+Gram–Schmidt is fp64, as in the reference (``reparameterize.py:195-197``)."""
 import torch
 
 from . import _lib
@@ -19,6 +21,19 @@ def _empty(shape, like, dtype=F32):
     return torch.empty(shape, device=like.device, dtype=dtype)
 
 
+F64 = torch.float64
+
+
+def _map_dtype(*ts):
+    """Compute dtype of a per-sample map: fp64 if any floating input is fp64 (torch's
+    promotion for the reference's expressions), else fp32."""
+    return F64 if any(t is not None and t.dtype == F64 for t in ts) else F32
+
+
+def _k(name, dtype):
+    return name + "_f64" if dtype == F64 else name
+
+
 def _flat(t, last):
     """View (..., *last) as (n, *last); returns the batch shape too."""
     lead = t.shape[: t.dim() - len(last)]
@@ -30,25 +45,27 @@ def _flat(t, last):
 
 # ------------------------------------------------------------- unary maps
 class _Unary(torch.autograd.Function):
-    """Generic per-sample map x (n, *IN) -> y (n, *OUT) with a VJP kernel."""
+    """Generic per-sample map x (n, *IN) -> y (n, *OUT) with a VJP kernel; fp32 or fp64
+    following the input."""
 
     @staticmethod
     def forward(ctx, x, spec):
         fwd, bwd, ishape, oshape = spec
-        xf, lead, n = _flat(_prep(x), ishape)
-        y = _empty((n, *oshape), xf)
-        call(fwd, ptr(xf), ptr(y), n, stream())
+        dt = _map_dtype(x) if fwd in _F64_MAPS else F32
+        xf, lead, n = _flat(_prep(x, dt), ishape)
+        y = _empty((n, *oshape), xf, dt)
+        call(_k(fwd, dt), ptr(xf), ptr(y), n, stream())
         ctx.save_for_backward(xf)
-        ctx.spec, ctx.lead, ctx.n = spec, lead, n
+        ctx.spec, ctx.lead, ctx.n, ctx.dt = spec, lead, n, dt
         return y.reshape(*lead, *oshape)
 
     @staticmethod
     def backward(ctx, gy):
         (xf,) = ctx.saved_tensors
         fwd, bwd, ishape, oshape = ctx.spec
-        gyf = _prep(gy).reshape(ctx.n, *oshape)
-        gx = _empty((ctx.n, *ishape), xf)
-        call(bwd, ptr(xf), ptr(gyf), ptr(gx), ctx.n, stream())
+        gyf = _prep(gy, ctx.dt).reshape(ctx.n, *oshape)
+        gx = _empty((ctx.n, *ishape), xf, ctx.dt)
+        call(_k(bwd, ctx.dt), ptr(xf), ptr(gyf), ptr(gx), ctx.n, stream())
         return gx.reshape(*ctx.lead, *ishape), None
 
 
@@ -58,6 +75,8 @@ MAT_TO_QUAT = ("lv_mat_to_quat_fwd", "lv_mat_to_quat_bwd", (3, 3), (4,))
 QUAT_TO_EAZYZ = ("lv_quat_to_eazyz_fwd", "lv_quat_to_eazyz_bwd", (4,), (3,))
 MAT_TO_EAZYZ = ("lv_mat_to_eazyz_fwd", "lv_mat_to_eazyz_bwd", (3, 3), (3,))
 SOFTPLUS = ("lv_softplus_fwd", "lv_softplus_bwd", (), ())
+# maps with fp64 twins
+_F64_MAPS = {s[0] for s in (SO3_EXP, QUAT_TO_MAT, MAT_TO_QUAT, QUAT_TO_EAZYZ, MAT_TO_EAZYZ)}
 
 
 def unary(x, spec):
@@ -68,20 +87,22 @@ def unary(x, spec):
 class _S2S1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, axis, cs):
-        a, lead, n = _flat(_prep(axis), (3,))
-        c, _, _ = _flat(_prep(cs), (2,))
-        r = _empty((n, 3, 3), a)
-        call("lv_s2s1_fwd", ptr(a), ptr(c), ptr(r), n, stream())
+        dt = _map_dtype(axis, cs)
+        a, lead, n = _flat(_prep(axis, dt), (3,))
+        c, _, _ = _flat(_prep(cs, dt), (2,))
+        r = _empty((n, 3, 3), a, dt)
+        call(_k("lv_s2s1_fwd", dt), ptr(a), ptr(c), ptr(r), n, stream())
         ctx.save_for_backward(a, c)
-        ctx.lead, ctx.n = lead, n
+        ctx.lead, ctx.n, ctx.dt = lead, n, dt
         return r.reshape(*lead, 3, 3)
 
     @staticmethod
     def backward(ctx, g):
         a, c = ctx.saved_tensors
-        gf = _prep(g).reshape(ctx.n, 3, 3)
-        ga, gc = _empty((ctx.n, 3), a), _empty((ctx.n, 2), a)
-        call("lv_s2s1_bwd", ptr(a), ptr(c), ptr(gf), ptr(ga), ptr(gc), ctx.n, stream())
+        gf = _prep(g, ctx.dt).reshape(ctx.n, 3, 3)
+        ga, gc = _empty((ctx.n, 3), a, ctx.dt), _empty((ctx.n, 2), a, ctx.dt)
+        call(_k("lv_s2s1_bwd", ctx.dt), ptr(a), ptr(c), ptr(gf), ptr(ga), ptr(gc), ctx.n,
+             stream())
         return ga.reshape(*ctx.lead, 3), gc.reshape(*ctx.lead, 2)
 
 
@@ -111,22 +132,25 @@ class _SO3Sample(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mu, v):
-        mu = _prep(mu)
-        v = _prep(v)
+        dt = _map_dtype(mu, v)
+        mu = _prep(mu, dt)
+        v = _prep(v, dt)
         ns, B = v.shape[0], v.shape[1]
         assert mu.shape == (B, 3, 3) and v.shape == (ns, B, 3)
-        z = _empty((ns, B, 3, 3), v)
-        call("lv_so3_sample_fwd", ptr(mu), ptr(v), ptr(z), ns, B, stream())
+        z = _empty((ns, B, 3, 3), v, dt)
+        call(_k("lv_so3_sample_fwd", dt), ptr(mu), ptr(v), ptr(z), ns, B, stream())
         ctx.save_for_backward(mu, v)
+        ctx.dt = dt
         return z
 
     @staticmethod
     def backward(ctx, gz):
         mu, v = ctx.saved_tensors
         ns, B = v.shape[0], v.shape[1]
-        gz = _prep(gz)
+        gz = _prep(gz, ctx.dt)
         gmu, gv = torch.empty_like(mu), torch.empty_like(v)
-        call("lv_so3_sample_bwd", ptr(mu), ptr(v), ptr(gz), ptr(gmu), ptr(gv), ns, B, stream())
+        call(_k("lv_so3_sample_bwd", ctx.dt), ptr(mu), ptr(v), ptr(gz), ptr(gmu), ptr(gv), ns,
+             B, stream())
         return gmu, gv
 
 

@@ -535,3 +535,69 @@ def test_vae_toy_elbo_and_log_likelihood_vs_oracle(gpu_device):
     w = -recon2 - math.log(8 * math.pi ** 2) - lq2
     ll_ref = (torch.logsumexp(w, 0) - math.log(n)).mean()
     np.testing.assert_allclose(float(ll), float(ll_ref), rtol=1e-4)
+
+
+# ---------------------------------------------------------------- fp64 inputs (a2-a6)
+def test_fp64_maps_follow_input_dtype(gpu_device):
+    """The reference's per-sample maps return the input dtype (lie_tools.py:28-38,61:
+    v.new_tensor, eye(dtype=v.dtype)) and its self-tests run them in fp64
+    (lie_tools.py:271-291).  fp64 in -> the *_f64 kernels: fp64 out, within 1e-12 of the
+    oracle's fp64 restatement, gradients within 1e-10 of its autograd; the reference's
+    own log/exp round-trip self-test (test_log_exp, lie_tools.py:280-291) in fp64."""
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    from oracle import lie_ref
+    torch.manual_seed(21)
+    n = 2000
+    f64 = torch.float64
+    v = torch.randn(n, 3, dtype=f64) * 1.3
+    q = lie_ref.haar_quaternions(n, dtype=f64)
+    r = lie_ref.quat_to_mat(q)
+    ax = torch.nn.functional.normalize(torch.randn(n, 3, dtype=f64), dim=-1)
+    th = torch.rand(n, dtype=f64) * 6.0
+    cs = torch.stack((torch.cos(th), torch.sin(th)), -1)
+    mu = lie_ref.haar_matrices(n, dtype=f64)
+    cases = [
+        ("rodrigues", lambda x: lt.rodrigues(x[0]), lambda x: lie_ref.so3_exp(x[0]), [v]),
+        ("quat_to_mat", lambda x: lt.quaternions_to_group_matrix(x[0]),
+         lambda x: lie_ref.quat_to_mat(x[0]), [q]),
+        ("mat_to_quat", lambda x: lt.group_matrix_to_quaternions(x[0]),
+         lambda x: lie_ref.mat_to_quat(x[0]), [r]),
+        ("quat_to_eazyz", lambda x: lt.quaternions_to_eazyz(x[0]),
+         lambda x: lie_ref.quat_to_eazyz(x[0]), [q]),
+        ("mat_to_eazyz", lambda x: lt.group_matrix_to_eazyz(x[0]),
+         lambda x: lie_ref.mat_to_eazyz(x[0]), [r]),
+        ("s2s1", lambda x: lt.s2s1rodrigues(x[0], x[1]), lambda x: lie_ref.s2s1_exp(x[0], x[1]),
+         [ax, cs]),
+        ("so3_sample", lambda x: ops.so3_sample(x[0], x[1][None])[0],
+         lambda x: lie_ref.so3_sample(x[0], x[1]), [mu, v]),
+    ]
+    for name, f, ref, xs in cases:
+        xg = [t.to(gpu_device).requires_grad_(True) for t in xs]
+        y = f(xg)
+        assert y.dtype == f64, (name, y.dtype)
+        xc = [t.clone().requires_grad_(True) for t in xs]
+        yr = ref(xc)
+        err = (host(y) - yr.detach().numpy())
+        scale = np.abs(yr.detach().numpy()).max()
+        # Euler extraction is ill-conditioned near beta = 0: a 1-ulp change of q moves the
+        # angles by far more than 1 ulp, so those maps get a looser (still fp64) bound
+        tol = 1e-9 if "eazyz" in name else 1e-12
+        assert np.abs(err).max() <= tol * max(scale, 1.0), (name, np.abs(err).max())
+        g = torch.randn(yr.shape, dtype=f64)
+        (y * g.to(gpu_device)).sum().backward()
+        (yr * g).sum().backward()
+        for a, b in zip(xg, xc):
+            assert a.grad.dtype == f64
+            ga, gb = host(a.grad), b.grad.numpy()
+            assert np.abs(ga - gb).max() <= (1e-7 if "eazyz" in name else 1e-10) * \
+                max(np.abs(gb).max(), 1.0), (name, np.abs(ga - gb).max())
+    # the reference's own self-test, fp64: rodrigues / log_map round trip at its
+    # tolerances (test_log_exp(0.1, 1E-6), test_log_exp(10, 1E-6), lie_tools.py:442-443)
+    for scale, tol in ((0.1, 1e-6), (10.0, 1e-6)):
+        vs = torch.randn(50, 3, dtype=f64, device=gpu_device) * scale
+        for k in range(50):
+            R = lt.rodrigues(vs[k])
+            w = lt.map_to_lie_vector(lt.log_map(R))
+            R2 = lt.rodrigues(w)
+            np.testing.assert_allclose(host(R2), host(R), rtol=tol, atol=tol)
