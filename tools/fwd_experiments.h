@@ -703,3 +703,99 @@ __global__ __launch_bounds__(512) void tile5_kernel(ActionArgs a) {
   }
 }
 }  // namespace lv
+
+namespace lv {
+// Two-phase tile kernel (experiment): the block first computes degrees [0, L1) (phase A,
+// split over its waves by seg_lo[0..nseg]), writes the rows [0, L1^2) of its samples
+// (Sv runs, 8-byte stores) and, while those stores drain, computes degrees [L1, L]
+// (phase B, seg_lo[nseg+1 .. 2 nseg+1]), then writes rows [L1^2, M).  Otherwise the
+// library tile kernel (prologue once per (sample, slot), whole spectrum in LDS).
+template <typename OutT, int POL>
+__device__ __forceinline__ void flush_rows(OutT* gout, const char* stage_b, int Sv, int MC,
+                                           int e0, int e1, int tid, int nthr) {
+  // elements [e0, e1) of each of the Sv samples (C even: pairs, 8-B aligned for fp32)
+  const int np = (e1 - e0) >> 1;
+  const float inv = 1.f / (float)np;
+  const int tot = Sv * np;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(gout, 0, Sv * MC * (int)sizeof(OutT), kRawBufferFlags);
+  for (int p = tid; p < tot; p += nthr) {
+    const int jj = (int)(((float)p + 0.5f) * inv), w = p - jj * np;
+    const int b = (jj * MC + e0 + 2 * w) * (int)sizeof(OutT);
+    const float2 v = *reinterpret_cast<const float2*>(stage_b + b);
+    st_b64<POL>(rs, b, v.x, v.y);
+  }
+}
+
+template <int LT, int POL>
+__global__ __launch_bounds__(512) void tile6_kernel(ActionArgs a) {
+  using OutT = float;
+  constexpr int CT = 10;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int kRow = TrigLds<LT>::kRow;
+  constexpr int C = CT, Sw = 64 / CT;
+  constexpr int MC = (LT + 1) * (LT + 1) * CT;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nseg = (int)(blockDim.x >> 6);
+  const int j = lane / C;
+  const int c = lane - j * C;
+  const int loA = a.seg_lo[wave], hiA = a.seg_lo[wave + 1];
+  const int loB = a.seg_lo[nseg + 1 + wave], hiB = a.seg_lo[nseg + 2 + wave];
+  const int L1 = a.seg_lo[nseg];
+  const int64_t s0 = (int64_t)blockIdx.x * Sw;
+  const int Sv = (int)min((int64_t)Sw, a.n - s0);
+  const bool active = j < Sv;
+  const int stage_bytes = tile_stage_bytes(Sw, MC, 4);
+  float* trig = lds + (stage_bytes >> 2);
+  float* Fs = trig + Sw * kRow;  // whole F row-major
+  const int tid = (int)threadIdx.x;
+  const bool task = tid < 3 * Sw;
+  const int jt = tid / 3, q = tid - 3 * (tid / 3);
+  const int64_t st = s0 + min(jt, Sv - 1);
+  LaneIn in;
+  if (task) lane_load<true>(a, st, in);
+  // stage both of this wave's spectrum slices
+  for (int e = loA * loA * C + lane; e < hiA * hiA * C; e += 64) Fs[e] = a.F[e];
+  for (int e = loB * loB * C + lane; e < hiB * hiB * C; e += 64) Fs[e] = a.F[e];
+  if (task) {
+    float c1[3], s1[3];
+    lane_angles<true>(a, in, st, jt < Sv, q, a.ang_out != nullptr, c1, s1);
+    trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
+  }
+  block_sync_lds();
+  float* gout = reinterpret_cast<float*>(a.out) + s0 * MC;
+  const int mis = (int)(reinterpret_cast<uintptr_t>(gout) & 15);
+  char* stage_b = reinterpret_cast<char*>(lds) + mis;
+  float* st_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
+  const float* tj = trig + min(j, Sw - 1) * kRow;
+  const float* Fl = Fs + c;
+  sfor<LT + 1>([&](auto Lc) {
+    constexpr int l = LV_CV(Lc);
+    if (l == L1) {  // phase A done: publish and write its rows, then phase B
+      block_sync_lds();
+      flush_rows<float, POL>(gout, stage_b, Sv, MC, 0, L1 * L1 * C, tid, (int)blockDim.x);
+    }
+    if ((l >= loA && l < hiA) || (l >= loB && l < hiB)) {
+      constexpr int nn = 2 * l + 1;
+      constexpr int r0 = l * l;
+      float x[nn], y[nn];
+      sfor<nn>([&](auto K) { x[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * C]; });
+      xrot_lds<l, 2, LT>(tj, x, y);
+      jmul<l>(y, x);
+      xrot_lds<l, 1, LT>(tj, x, y);
+      jmul<l>(y, x);
+      xrot_lds<l, 0, LT>(tj, x, y);
+      if (active) {
+        float* d = st_lane + r0 * C;
+        sfor<nn>([&](auto I) {
+          d[0] = y[LV_CV(I)];
+          d += C;
+        });
+      }
+    }
+  });
+  block_sync_lds();
+  flush_rows<float, POL>(gout, stage_b, Sv, MC, L1 * L1 * C, MC, tid, (int)blockDim.x);
+}
+}  // namespace lv

@@ -137,6 +137,35 @@ int main(int argc, char** argv) {
   lib_tile(4, 1, true);
   for (int nseg : {3, 4, 5, 6, 7, 8})
     printf("n=%lld lib tile nseg=%d: sc1 %8.2f us  nt %8.2f us\n", (long long)n, nseg, lib_tile(nseg, 1, false), lib_tile(nseg, 0, false));
+  // two-phase tile kernel: degrees [0, L1) then [L1, L], the first part's rows written
+  // while the second part computes
+  auto plan_range = [&](int lo, int hi, int nseg, int* seg) {
+    auto nnz = nnz_tab(std::make_integer_sequence<int, L + 1>{});
+    std::vector<double> cost;
+    for (int l = lo; l < hi; ++l) cost.push_back(2.0 * nnz[l] + 12.0 * l + 10.0);
+    double tot = 0; for (double x : cost) tot += x;
+    int k = 0; double acc = 0; seg[0] = lo;
+    for (int l = lo; l < hi && k < nseg - 1; ++l) {
+      acc += cost[l - lo];
+      if (acc >= tot * (k + 1) / nseg) { seg[++k] = l + 1; }
+    }
+    while (k < nseg - 1) { seg[k + 1] = seg[k]; ++k; }
+    seg[nseg] = hi;
+  };
+  for (int L1 : {6, 7, 8})
+    for (int nseg : {4, 5, 6, 7}) {
+      ActionArgs b = a;
+      plan_range(0, L1, nseg, b.seg_lo);
+      plan_range(L1, L + 1, nseg, b.seg_lo + nseg + 1);
+      const size_t l6 = tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)b.MC + (size_t)b.Sw * TrigLds<L>::kRow);
+      const dim3 g(gx), bl(64 * nseg);
+      const size_t bad = check(tile6_kernel<L, 16>, g, bl, l6, b, n, ref);
+      const double t16 = timeit(tile6_kernel<L, 16>, g, bl, l6, b, reps);
+      const double t1 = timeit(tile6_kernel<L, 1>, g, bl, l6, b, reps);
+      printf("n=%lld two-phase L1=%d nseg=%d: sc1 %8.2f  nt %8.2f us  %s\n", (long long)n, L1, nseg, t16, t1,
+             bad ? "MISMATCH" : "bitwise-ok");
+    }
+  return 0;
   // tile v5: trig from LDS per degree (TM 1), per-wave flush (FM 1)
   auto t5 = [&](auto tm, auto fm, int nseg, const char* tag) {
     constexpr int TM = decltype(tm)::value, FM = decltype(fm)::value;
