@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.join(REPO, "lie-vae_amd"))
 from lie_vae.experiments import launch  # noqa: E402  (no HIP call at import)
 
 F32_PEAK_TFLOPS = 157.3  # MI355X f32 MFMA = f32 VALU (v_pk_fma_f32) peak, MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
 
 
 def main():
@@ -43,6 +44,9 @@ def main():
     ap.add_argument("--deconv-hidden", type=int, default=200)
     ap.add_argument("--mean-mode", default="s2s2")
     ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--amp", choices=["off", "bf16"], default="off",
+                    help="bf16 autocast for the conv / deconv / linear layers (fp32 master "
+                         "weights; the SO(3) kernels stay fp32)")
     ap.add_argument("--no-find", dest="find", action="store_false",
                     help="keep MIOpen's heuristic conv solutions (default: torch.backends."
                          "cudnn.benchmark, MIOpen times the candidates once per shape)")
@@ -79,7 +83,8 @@ def main():
                 mean_mode=args.mean_mode).to(dev)
     if args.channels_last:
         model = model.to(memory_format=torch.channels_last)
-    trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5)
+    trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5,
+                        amp_dtype=torch.bfloat16 if args.amp == "bf16" else None)
     B = args.global_batch // world
     g = torch.Generator(device="cpu").manual_seed(100 + rank)
     x = torch.rand(B, 3, 64, 64, generator=g).to(dev)
@@ -107,6 +112,7 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
+    peak = F32_PEAK_TFLOPS if args.amp == "off" else BF16_PEAK_TFLOPS
     if rank == 0:
         print(json.dumps({
             "metric": "VAE train samples/s (conv enc + SO(3) reparam + action dec, l=10)",
@@ -114,12 +120,13 @@ def main():
             "steps": args.steps, "ms_per_step": el * 1e3 / args.steps,
             "config": {"global_batch": args.global_batch, "per_gpu": B, "l_max": args.lmax,
                        "deconv_hidden": args.deconv_hidden, "mean_mode": args.mean_mode,
-                       "params": param_count(model), "dtype": "f32",
+                       "params": param_count(model),
+                       "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,
-                       "peak_tflops": F32_PEAK_TFLOPS,
-                       "frac": step_flops / (el / args.steps) / 1e12 / F32_PEAK_TFLOPS},
+                       "peak_tflops": peak,
+                       "frac": step_flops / (el / args.steps) / 1e12 / peak},
             "loss": float(loss.item()), "recon": float(recon.mean().item()),
             "kl": float(kl.mean().item())}), flush=True)
     if world > 1:

@@ -129,12 +129,20 @@ class DPTrainer:
       * Adam step.
     The per-step NaN-KL check (unsupervised.py:97-98) forces a host sync; it is off by
     default and enabled with ``nan_check=True``.
+
+    ``amp_dtype=torch.bfloat16`` runs the forward under autocast: the conv encoder,
+    deconv decoder and linear layers compute on the bf16 MFMA path (fp32 accumulate, fp32
+    master weights and Adam state), while the SO(3) kernels keep computing in fp32 (their
+    autograd ops cast their inputs) and S2S2 in fp64.  Off by default: the reference
+    trains in fp32.
     """
 
     def __init__(self, model, lr=1e-3, weight_decay=0.0, clip_grads=1e-5, beta=1.0,
                  elbo_samples=1, bucket_bytes=32 << 20, group=None, broadcast=True,
-                 control=None, control_p=1, selective_clip=False, nan_check=False):
+                 control=None, control_p=1, selective_clip=False, nan_check=False,
+                 amp_dtype=None):
         self.model = model
+        self.amp_dtype = amp_dtype
         self.clip = clip_grads
         self.beta_schedule = beta if callable(beta) else ConstantSchedule(beta)
         self.n = elbo_samples
@@ -151,6 +159,15 @@ class DPTrainer:
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
 
     def loss(self, x, eps=None, beta=1.0):
+        if self.amp_dtype is not None:
+            with torch.autocast(device_type=x.device.type, dtype=self.amp_dtype):
+                out = self._loss(x, eps, beta)
+            # autocast may leave bf16 reductions; the fp32/fp64 terms keep their dtype
+            return tuple(t.float() if t.dtype in (torch.bfloat16, torch.float16) else t
+                         for t in out)
+        return self._loss(x, eps, beta)
+
+    def _loss(self, x, eps=None, beta=1.0):
         if beta == 0:
             x_recon = self.model.forward(x, self.n, eps=eps)
             recon = self.model.recon_loss(x_recon, x)

@@ -268,3 +268,29 @@ def test_vae_fused_decode_matches_modular(gpu_device):
     for k in outs[0][1]:
         assert_normwise(host(outs[0][1][k]).reshape(1, -1), host(outs[1][1][k]).reshape(1, -1),
                         1e-4, what=f"grad {k}")
+
+
+def test_dp_trainer_bf16_autocast_step(gpu_device):
+    """DPTrainer(amp_dtype=bf16): the convs run under autocast while the SO(3) kernels
+    stay fp32 (their ops cast); two steps are finite and move the loss like fp32 does
+    to within bf16 noise."""
+    from lie_vae.experiments.train_dp import DPTrainer
+    from lie_vae.experiments.vae import VAE
+    torch.manual_seed(0)
+    base = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10, rgb=True,
+               batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(gpu_device)
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(64, 3, 64, 64, generator=g).to(gpu_device)
+    eps = torch.randn(1, 64, 3, generator=g).to(gpu_device)
+    out = {}
+    for amp in (None, torch.bfloat16):
+        m = copy.deepcopy(base)
+        tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5, amp_dtype=amp)
+        l1, r1, k1 = tr.step(x, eps)
+        l2, _, _ = tr.step(x, eps)
+        torch.cuda.synchronize()
+        assert l1.dtype in (torch.float32, torch.float64)
+        assert torch.isfinite(l1) and torch.isfinite(l2)
+        assert all(torch.isfinite(p).all() for p in m.parameters())
+        out[amp] = (float(l1), float(l2))
+    assert out[torch.bfloat16][0] == pytest.approx(out[None][0], rel=2e-2)
