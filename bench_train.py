@@ -14,6 +14,12 @@ available offline), seeded per rank.
   python bench_train.py                                   # config 3
   python bench_train.py --gpus 8 --global-batch 4096      # config 4 (spawns 8 ranks)
   python bench_train.py --gpus 2 --dry-run                # rank plumbing on CPU (gloo)
+  python bench_train.py --iwae 64                         # IWAE LL eval, n=500 (f3)
+
+``--iwae K`` times the reference's evaluation instead (main.py:134-139): the importance-
+weighted log-likelihood with n = 500 samples over K test images, once one image per call
+as the reference's batch-1 loader does, once ``--iwae-batch`` images per call; images
+are sharded over ranks.
 
 ``--gpus N`` without a torch.distributed environment hands the script to
 torch.distributed.run before any HIP call (lie_vae/experiments/launch.py).
@@ -50,6 +56,10 @@ def main():
     ap.add_argument("--no-find", dest="find", action="store_false",
                     help="keep MIOpen's heuristic conv solutions (default: torch.backends."
                          "cudnn.benchmark, MIOpen times the candidates once per shape)")
+    ap.add_argument("--iwae", type=int, default=0, metavar="K",
+                    help="time the IWAE log-likelihood (n=500) over K images instead")
+    ap.add_argument("--iwae-n", type=int, default=500)
+    ap.add_argument("--iwae-batch", type=int, default=8)
     ap.add_argument("--dry-run", action="store_true",
                     help="rehearse the rank plumbing on CPU (gloo, no HIP call)")
     args = ap.parse_args()
@@ -83,6 +93,8 @@ def main():
                 mean_mode=args.mean_mode).to(dev)
     if args.channels_last:
         model = model.to(memory_format=torch.channels_last)
+    if args.iwae:
+        return bench_iwae(args, model, env, dev)
     trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5,
                         amp_dtype=torch.bfloat16 if args.amp == "bf16" else None)
     B = args.global_batch // world
@@ -129,6 +141,52 @@ def main():
                        "frac": step_flops / (el / args.steps) / 1e12 / peak},
             "loss": float(loss.item()), "recon": float(recon.mean().item()),
             "kl": float(kl.mean().item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_iwae(args, model, env, dev):
+    """IWAE evaluation throughput (images/s) at n = args.iwae_n: the reference's one-image
+    calls, then args.iwae_batch images per call (same per-image terms)."""
+    import torch.distributed as dist
+    world, rank = env.world, env.rank
+    # MIOpen's find on the n*B-image deconv shapes takes minutes per shape; the
+    # evaluation runs each shape only K/B times, so it keeps the heuristic solutions
+    torch.backends.cudnn.benchmark = False
+    K = args.iwae // world
+    g = torch.Generator(device="cpu").manual_seed(200 + rank)
+    x = torch.rand(K, 3, 64, 64, generator=g).to(dev)
+    model.eval()
+    res = {}
+    with torch.no_grad():
+        for tag, bs in (("batch1", 1), (f"batch{args.iwae_batch}", args.iwae_batch)):
+            for i in range(0, min(K, 2 * bs), bs):  # warm-up (MIOpen find per shape)
+                model.log_likelihood(x[i:i + bs], n=args.iwae_n)
+                torch.cuda.synchronize(dev)
+                print(f"[iwae] {tag}: warm-up call done", file=sys.stderr, flush=True)
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            lls = [model.log_likelihood(x[i:i + bs], n=args.iwae_n) * x[i:i + bs].shape[0]
+                   for i in range(0, K, bs)]
+            ll = torch.stack(lls).sum()
+            torch.cuda.synchronize(dev)
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                dist.all_reduce(ll)
+            res[tag] = {"images_per_call": bs, "images_per_s": K * world / float(el.item()),
+                        "ms_per_image": float(el.item()) * 1e3 / K,
+                        "mean_ll": float(ll.item()) / (K * world)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"IWAE log-likelihood eval images/s (n={args.iwae_n})",
+            "value": res[f"batch{args.iwae_batch}"]["images_per_s"], "unit": "images/s",
+            "n_gpus": world, "images": K * world,
+            "config": {"l_max": args.lmax, "deconv_hidden": args.deconv_hidden,
+                       "mean_mode": args.mean_mode, "dtype": "f32",
+                       "data": "synthetic x ~ U[0,1), random-init weights"},
+            "runs": res}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

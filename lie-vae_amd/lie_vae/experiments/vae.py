@@ -109,9 +109,14 @@ class VAE(nn.Module):
         kl_summed = torch.sum(torch.stack(kl, -1), -1)
         return self.recon_loss(x_recon, x), kl_summed, kl
 
-    def log_likelihood(self, x, n=1):
-        """Importance-weighted log-likelihood (vae.py:164-171)."""
-        x_recon = self.forward(x, n)
+    def log_likelihood(self, x, n=1, eps=None):
+        """Importance-weighted log-likelihood (vae.py:164-171), averaged over the batch.
+
+        The reference evaluates it one image at a time with n = 500 (main.py:134-139);
+        any batch gives the same per-image terms, so a caller can evaluate many test
+        images per launch.  ``eps`` (n, B, 3) optionally injects the latent noise (the
+        reference always draws it; ``None`` keeps that)."""
+        x_recon = self.forward(x, n, eps=eps)
         log_p_z = torch.cat([r.log_prior() for r in self.reparameterize], -1).to(x.device)
         log_q_z_x = torch.cat([r.log_posterior() for r in self.reparameterize], -1).to(x.device)
         log_p_x_z = -self.recon_loss(x_recon, x)

@@ -294,3 +294,44 @@ def test_dp_trainer_bf16_autocast_step(gpu_device):
         assert all(torch.isfinite(p).all() for p in m.parameters())
         out[amp] = (float(l1), float(l2))
     assert out[torch.bfloat16][0] == pytest.approx(out[None][0], rel=2e-2)
+
+
+def test_config3_iwae_n500_vs_oracle(gpu_device):
+    """The reference's evaluation (main.py:134-139): IWAE log-likelihood with n = 500 on
+    the conv VAE, one image per call.  The SO(3) terms (log q over the 500 samples, the
+    fused decode) against the oracle fed the GPU encoder features and the same eps; the
+    recon term from the GPU deconv output (MIOpen vs CPU is checked in the config-3 test).
+    A 2-image call gives the mean of the two 1-image calls (same eps slices)."""
+    from lie_vae.experiments.vae import VAE
+    from oracle import lie_ref
+    L, C, n = 10, 10, 500
+    torch.manual_seed(5)
+    cpu = VAE(latent_mode="so3", decoder_mode="action", degrees=L, rep_copies=C, rgb=True,
+              batch_norm=True, deconv_hidden=200, mean_mode="s2s2").eval()
+    gvae = copy.deepcopy(cpu).to(gpu_device).eval()
+    g = torch.Generator().manual_seed(6)
+    x = torch.rand(2, 3, 64, 64, generator=g)
+    eps = torch.randn(n, 2, 3, generator=g)
+    lls = []
+    rep = cpu.rep_group
+    for b in range(2):
+        cap = {}
+        hooks = [_capture(gvae.encoder, cap, "enc"), _capture(gvae.decoder.deconv, cap, "dec")]
+        with torch.no_grad():
+            ll = gvae.log_likelihood(x[b:b + 1].to(gpu_device), n=n,
+                                     eps=eps[:, b:b + 1].to(gpu_device))
+        for h in hooks:
+            h.remove()
+        lls.append(float(ll))
+        h_gpu, xr_gpu = cap["enc"][1].cpu(), cap["dec"][1].cpu()
+        with torch.no_grad():
+            sig = lie_ref.n0_sigma(rep.reparameterize.sigma_linear(h_gpu))
+            vv = lie_ref.n0_sample(sig, eps[:, b:b + 1])
+            lq = lie_ref.so3_log_posterior(vv, sig, 10)                      # (n, 1)
+        rec = ((xr_gpu.reshape(n, 1, 3, 64, 64) - x[b:b + 1]) ** 2).sum((-1, -2, -3))
+        w = (-rec - math.log(8 * math.pi ** 2) - lq).double()
+        ll_ref = float((torch.logsumexp(w, 0) - math.log(n)).mean())
+        assert ll_ref == pytest.approx(lls[-1], rel=1e-5)
+    with torch.no_grad():
+        ll2 = gvae.log_likelihood(x.to(gpu_device), n=n, eps=eps.to(gpu_device))
+    assert float(ll2) == pytest.approx(sum(lls) / 2, rel=1e-5)
