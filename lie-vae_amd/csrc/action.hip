@@ -153,7 +153,8 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   if (a.C != kTileFastC && L < kTileFGlobalMinL)
     for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
   a.fpitch = (fp + 3) & ~3;
-  const size_t fl = a.C == kTileFastC ? (size_t)a.MC : (size_t)nseg * a.fpitch;
+  // (C = kTileFastC with fp32 output: the spectrum sits in the tile's last sample slot)
+  const size_t fl = a.C == kTileFastC ? (out_bytes == 4 ? 0 : (size_t)a.MC) : (size_t)nseg * a.fpitch;
   const size_t trig = (size_t)Sw * (6 * ((L + 1 + 3) & ~3) + 4);  // TrigLds<L>::kRow per sample
   const size_t lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) + sizeof(float) * (fl + trig);
   if (lds > kTileMaxLds || groups > 0x7fffffff) return false;

@@ -1,4 +1,5 @@
 #pragma once
+#include <type_traits>
 // Forward group-action kernels for gfx950 (MI355X) + their launchers.
 // Instantiated once per l_max in action_inst.hip (-DLV_INST_L=k) so the 21 degree
 // variants compile in parallel; host planning lives in action.hip.
@@ -260,6 +261,12 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kRow = TrigLds<LT>::kRow;
   constexpr bool FG = CT == 0 && LT >= kTileFGlobalMinL;  // spectrum from global, no LDS
+  // fp32 tile with compile-time C: the spectrum lives in the tile's LAST sample slot
+  // (same [row][c] layout, M*C floats).  A wave reads degree l's spectrum rows into
+  // registers before it writes that degree's tile rows, and no other wave touches those
+  // rows, so the slot is free to be overwritten; the block saves M*C*4 bytes of LDS
+  // (l = 10: 35.7 -> 30.9 KB, 4 -> 5 blocks per CU).
+  constexpr bool FT = CT > 0 && std::is_same_v<OutT, float>;
   const int C = CT > 0 ? CT : a.C;
   const int Sw = CT > 0 ? 64 / CT : a.Sw;
   const int64_t MC = CT > 0 ? (int64_t)(LT + 1) * (LT + 1) * CT : a.MC;
@@ -275,9 +282,13 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   const bool active = j < Sv;
   const int stage_bytes = tile_stage_bytes(Sw, MC, (int)sizeof(OutT));
   float* trig = lds + (stage_bytes >> 2);
-  // spectrum in LDS: CT > 0 the whole (M, C) row-major (each wave fills its rows), else
-  // per-wave column-major slices of a.fpitch floats
-  float* Fw = trig + Sw * kRow + (CT > 0 ? rows_lo * C : wave * a.fpitch);
+  OutT* gout = reinterpret_cast<OutT*>(a.out) + s0 * MC;
+  const int mis = (int)(reinterpret_cast<uintptr_t>(gout) & 15);
+  char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
+  // spectrum in LDS: CT > 0 the whole (M, C) row-major (each wave fills its rows; FT: in
+  // the tile's last sample slot), else per-wave column-major slices of a.fpitch floats
+  float* const Fall = FT ? reinterpret_cast<float*>(stage_b) + (Sw - 1) * MC : trig + Sw * kRow;
+  float* Fw = Fall + (CT > 0 ? rows_lo * C : wave * a.fpitch);
   // 1. prologue task (sample jt, slot q); the host guarantees 3*Sw <= blockDim.x
   const int tid = (int)threadIdx.x;
   const bool task = tid < 3 * Sw;
@@ -324,14 +335,10 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   }
   block_sync_lds();
 
-  OutT* gout = reinterpret_cast<OutT*>(a.out) + s0 * MC;
-  const int mis = (int)(reinterpret_cast<uintptr_t>(gout) & 15);
-  char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
   OutT* st_lane = reinterpret_cast<OutT*>(stage_b) + j * MC + c;
   const float* tj = trig + min(j, Sw - 1) * kRow;
   // spectrum column: LDS slice, or global (FG)
-  const float* Fl = FG ? a.F + c : (CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo);
-  // (CT > 0: Fw + c - rows_lo*C is the start of the block's full row-major copy + c)
+  const float* Fl = FG ? a.F + c : (CT > 0 ? Fall + c : Fw + c * frows - rows_lo);
   const int fstep = (FG || CT > 0) ? C : 1;  // stride between consecutive rows of a column
 
   sfor<LT + 1>([&](auto Lc) {

@@ -4,8 +4,9 @@
 // with HIP events.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
 //     -I lie-vae_amd/csrc tools/fwdbench.hip -o tools/kbench_fwd
-//   ./tools/kbench_fwd [n] [reps]
+//   ./tools/kbench_fwd [n] [reps] [occ]
 #include <algorithm>
+#include <string>
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -120,12 +121,12 @@ int main(int argc, char** argv) {
   }
   // reference + baseline: the library's tile kernel (C = 10 specialisation)
   std::vector<float> ref((size_t)n * M * C);
-  auto lib_tile = [&](int nseg, int wt, bool keep) {
+  auto lib_tile = [&](int nseg, int wt, bool keep, size_t pad = 0) {
     ActionArgs b = a;
     plan(nseg, 60.0, b.seg_lo);
     b.fpitch = fslice(b, nseg);
     b.write_through = wt;
-    const size_t lds = tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)b.MC + (size_t)b.Sw * TrigLds<L>::kRow);
+    const size_t lds = pad + tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)b.Sw * TrigLds<L>::kRow);  // spectrum in the tile
     Kern k = action_fwd_tile_kernel<L, C, true, float>;
     if (keep) {
       hipLaunchKernelGGL(k, dim3(gx), dim3(64 * nseg), lds, 0, b);
@@ -135,6 +136,18 @@ int main(int argc, char** argv) {
     return timeit(k, dim3(gx), dim3(64 * nseg), lds, b, reps);
   };
   lib_tile(4, 1, true);
+  if (argc > 3 && std::string(argv[3]) == "occ") {
+    // occupancy sensitivity: pad the block's LDS so fewer blocks fit per CU (160 KB)
+    const size_t base = tile_stage_bytes(a.Sw, a.MC, 4) + 4 * ((size_t)a.Sw * TrigLds<L>::kRow);
+    for (int per_cu : {5, 4, 2})
+      for (int nseg : {4, 5, 6}) {
+        const size_t want = 160 * 1024 / per_cu - 64;
+        const size_t pad = per_cu == 5 ? 0 : ((want - base) & ~(size_t)15);
+        printf("n=%lld occ blocks/CU<=%d (lds %zu) nseg=%d: sc1 %8.2f us  nt %8.2f us\n", (long long)n,
+               per_cu, base + pad, nseg, lib_tile(nseg, 1, false, pad), lib_tile(nseg, 0, false, pad));
+      }
+    return 0;
+  }
   for (int nseg : {3, 4, 5, 6, 7, 8})
     printf("n=%lld lib tile nseg=%d: sc1 %8.2f us  nt %8.2f us\n", (long long)n, nseg, lib_tile(nseg, 1, false), lib_tile(nseg, 0, false));
   // two-phase tile kernel: degrees [0, L1) then [L1, L], the first part's rows written

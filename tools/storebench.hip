@@ -38,7 +38,19 @@ __global__ void st_pieces80(float* o, int64_t n, int MC, int C) {
   const int rows = MC / C;
   for (int r = 0; r + 1 < rows; r += 2) { *reinterpret_cast<float2*>(d) = make_float2(r, r); d += 2 * C; }
 }
-// (e) same pieces but row pairs written as dwordx2 by lanes owning 2 columns (C/2 lanes per sample)
+// (e) the tile kernel's flush: block b writes its contiguous run of S samples (S*MC
+//     floats) with 16-B buffer stores, cache policy POL (0 default, 1 nt, 16 sc1)
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int POL>
+__global__ __launch_bounds__(1024) void st_chunk(float* o, int64_t n, int MC, int S) {
+  const int64_t s0 = (int64_t)blockIdx.x * S;
+  const int Sv = (int)min((int64_t)S, n - s0);
+  const int nbytes = Sv * MC * 4;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(o + s0 * MC, 0, nbytes, 0x00020000);
+  const float v = (float)blockIdx.x;
+  for (int k = threadIdx.x; k < nbytes / 16; k += blockDim.x)
+    __builtin_amdgcn_raw_buffer_store_b128(f4v{v, v, v, v}, r, 16 * k, 0, POL);
+}
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 65536;
   const int MC = 1210, C = 10;
@@ -68,5 +80,16 @@ int main(int argc, char** argv) {
   const int blocks = (int)((n + 23) / 24);
   run("pieces40B", [&] { hipLaunchKernelGGL(st_pieces, dim3(blocks), dim3(256), 0, 0, o, n, MC, C); });
   run("pieces80B float2", [&] { hipLaunchKernelGGL(st_pieces80, dim3(blocks), dim3(256), 0, 0, o, n, MC, C); });
+  for (int S : {6, 12, 24, 48})
+    for (int nw : {4, 8, 16}) {
+      const int g = (int)((n + S - 1) / S);
+      char nm[64];
+      snprintf(nm, 64, "chunk S=%d w=%d def", S, nw);
+      run(nm, [&] { hipLaunchKernelGGL(st_chunk<0>, dim3(g), dim3(64 * nw), 0, 0, o, n, MC, S); });
+      snprintf(nm, 64, "chunk S=%d w=%d nt", S, nw);
+      run(nm, [&] { hipLaunchKernelGGL(st_chunk<1>, dim3(g), dim3(64 * nw), 0, 0, o, n, MC, S); });
+      snprintf(nm, 64, "chunk S=%d w=%d sc1", S, nw);
+      run(nm, [&] { hipLaunchKernelGGL(st_chunk<16>, dim3(g), dim3(64 * nw), 0, 0, o, n, MC, S); });
+    }
   return 0;
 }
