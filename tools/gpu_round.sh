@@ -27,7 +27,7 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --sweep
   step bench_c5 600 python bench.py --lmax 20 --batch 8192 --dtype bf16 --no-cpu-baseline --steps 500
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline --multistream 1
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline --multistream 1 --cold-launches 0 --no-fwd-bwd
   rm -f "$OUT"/prof/*kernel_trace.csv
 fi
 if [ "$MODE" = all ] || [ "$MODE" = train ]; then
