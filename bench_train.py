@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--no-find", dest="find", action="store_false",
                     help="keep MIOpen's heuristic conv solutions (default: torch.backends."
                          "cudnn.benchmark, MIOpen times the candidates once per shape)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole step (fwd, bwd, all-reduce, clip, Adam) in a "
+                         "hipGraph and time its replays")
     ap.add_argument("--iwae", type=int, default=0, metavar="K",
                     help="time the IWAE log-likelihood (n=500) over K images instead")
     ap.add_argument("--iwae-n", type=int, default=500)
@@ -96,7 +99,8 @@ def main():
     if args.iwae:
         return bench_iwae(args, model, env, dev)
     trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5,
-                        amp_dtype=torch.bfloat16 if args.amp == "bf16" else None)
+                        amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
+                        graph=args.graph)
     B = args.global_batch // world
     g = torch.Generator(device="cpu").manual_seed(100 + rank)
     x = torch.rand(B, 3, 64, 64, generator=g).to(dev)
@@ -109,13 +113,14 @@ def main():
     with FlopCounterMode(display=False) as fc:
         trainer.step(x)
     step_flops = fc.get_total_flops()
+    run = trainer.capture(x) if args.graph else (lambda: trainer.step(x))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss, recon, kl = trainer.step(x)
+        loss, recon, kl = run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -134,7 +139,8 @@ def main():
                        "deconv_hidden": args.deconv_hidden, "mean_mode": args.mean_mode,
                        "params": param_count(model),
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
-                       "channels_last": args.channels_last, "miopen_find": args.find},
+                       "channels_last": args.channels_last, "miopen_find": args.find,
+                       "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,
                        "peak_tflops": peak,

@@ -135,12 +135,16 @@ class DPTrainer:
     master weights and Adam state), while the SO(3) kernels keep computing in fp32 (their
     autograd ops cast their inputs) and S2S2 in fp64.  Off by default: the reference
     trains in fp32.
+
+    ``graph=True`` builds Adam with device-side step state (``capturable``) so that
+    :meth:`capture` can record the whole step -- forward, backward, the bucketed
+    all-reduce, clip and Adam -- as one hipGraph and replay it without host launches.
     """
 
     def __init__(self, model, lr=1e-3, weight_decay=0.0, clip_grads=1e-5, beta=1.0,
                  elbo_samples=1, bucket_bytes=32 << 20, group=None, broadcast=True,
                  control=None, control_p=1, selective_clip=False, nan_check=False,
-                 amp_dtype=None):
+                 amp_dtype=None, graph=False):
         self.model = model
         self.amp_dtype = amp_dtype
         self.clip = clip_grads
@@ -156,11 +160,15 @@ class DPTrainer:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, src=0, group=group)
         self.ar = BucketedAllReduce(model.parameters(), bucket_bytes=bucket_bytes, group=group)
-        self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay,
+                                    capturable=graph)
+        self._graph = None
 
     def loss(self, x, eps=None, beta=1.0):
         if self.amp_dtype is not None:
-            with torch.autocast(device_type=x.device.type, dtype=self.amp_dtype):
+            # no autocast weight cache: the step may be captured into a graph
+            with torch.autocast(device_type=x.device.type, dtype=self.amp_dtype,
+                                cache_enabled=False):
                 out = self._loss(x, eps, beta)
             # autocast may leave bf16 reductions; the fp32/fp64 terms keep their dtype
             return tuple(t.float() if t.dtype in (torch.bfloat16, torch.float16) else t
@@ -190,7 +198,9 @@ class DPTrainer:
 
     def step(self, x, eps=None):
         self.it += 1
-        beta = self.beta_schedule(self.it)
+        return self._step_body(x, eps, self.beta_schedule(self.it))
+
+    def _step_body(self, x, eps, beta):
         self.ar.zero_grad()
         loss, recon, kl = self.loss(x, eps, beta)
         if self.nan_check and torch.isnan(kl).sum():
@@ -201,6 +211,66 @@ class DPTrainer:
             torch.nn.utils.clip_grad_norm_(self.clip_params(), self.clip)
         self.opt.step()
         return loss.detach(), recon.detach(), kl.detach()
+
+    # ------------------------------------------------------------ graph capture
+    def _state_tensors(self):
+        ts = list(self.model.parameters()) + list(self.model.buffers())
+        for p in self.model.parameters():
+            ts += [t for t in self.opt.state.get(p, {}).values() if torch.is_tensor(t)]
+        return ts
+
+    def capture(self, x, eps=None, warmup=3):
+        """Record one training step as a hipGraph; returns ``replay(x=None, eps=None)``
+        which copies new inputs into the graph's static buffers, replays the step and
+        returns its (loss, recon, kl) tensors (overwritten by the next replay).
+
+        The warm-up steps that capture needs (allocator pools, MIOpen solutions, lazy
+        Adam state) run on a side stream and are then undone: parameters, buffers and
+        optimizer state are restored in place, so the first replay is the step eager
+        ``step`` would have taken from the same state.  Needs ``graph=True``, a constant
+        non-zero beta and ``nan_check=False`` (the graph has no host branch)."""
+        if not self.opt.defaults.get("capturable"):
+            raise ValueError("capture() needs DPTrainer(graph=True) (capturable Adam)")
+        if not isinstance(self.beta_schedule, ConstantSchedule) or self.beta_schedule.value == 0:
+            raise ValueError("capture() needs a constant, non-zero beta")
+        if self.nan_check:
+            raise ValueError("capture() cannot run the per-step NaN check")
+        beta = self.beta_schedule.value
+        dev = x.device
+        gx = x.detach().clone()
+        geps = None if eps is None else eps.detach().clone()
+        had_state = {p for p in self.model.parameters() if self.opt.state.get(p)}
+        snap = [(t, t.detach().clone()) for t in self._state_tensors()]
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._step_body(gx, geps, beta)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self._step_body(gx, geps, beta)
+        torch.cuda.synchronize(dev)
+        # undo warm-up + capture: the tensors that existed before, then fresh Adam state
+        with torch.no_grad():
+            for t, v in snap:
+                t.copy_(v)
+            for p in self.model.parameters():
+                if p not in had_state:
+                    for t in self.opt.state.get(p, {}).values():
+                        if torch.is_tensor(t):
+                            t.zero_()
+        self._graph = graph
+
+        def replay(x_new=None, eps_new=None):
+            if x_new is not None:
+                gx.copy_(x_new)
+            if eps_new is not None:
+                geps.copy_(eps_new)
+            self.it += 1
+            graph.replay()
+            return out
+        return replay
 
 
 def shard(batch, rank, world):

@@ -213,7 +213,9 @@ class SO3reparameterize(nn.Module):
         return _ops.so3_log_posterior(v, sigma, self.k)
 
     def log_prior(self):
-        prior = torch.tensor([- np.log(8 * (np.pi ** 2))], device=self.z.device)
+        # = torch.tensor([-log 8pi^2], device=...) (reparameterize.py:265-267) without the
+        # host-to-device copy, so the step stays capturable in a hipGraph
+        prior = self.z.new_full((1,), - np.log(8 * (np.pi ** 2)), dtype=torch.get_default_dtype())
         return prior.expand_as(self.z[..., 0, 0])
 
     def nsample(self, n=1):

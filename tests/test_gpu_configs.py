@@ -335,3 +335,39 @@ def test_config3_iwae_n500_vs_oracle(gpu_device):
     with torch.no_grad():
         ll2 = gvae.log_likelihood(x.to(gpu_device), n=n, eps=eps.to(gpu_device))
     assert float(ll2) == pytest.approx(sum(lls) / 2, rel=1e-5)
+
+
+def test_dp_trainer_graph_replay_matches_eager(gpu_device):
+    """DPTrainer.capture: the whole step (forward, backward, all-reduce, clip, capturable
+    Adam) as one hipGraph.  Its warm-up is undone, so replays from a model's state follow
+    the same trajectory as eager steps from a copy of that state (MIOpen pinned
+    deterministic; eps injected)."""
+    from lie_vae.experiments.train_dp import DPTrainer
+    from lie_vae.experiments.vae import VAE
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        torch.manual_seed(0)
+        base = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10,
+                   rgb=True, batch_norm=True, deconv_hidden=200,
+                   mean_mode="s2s2").to(gpu_device)
+        g = torch.Generator().manual_seed(4)
+        xs = [torch.rand(64, 3, 64, 64, generator=g).to(gpu_device) for _ in range(3)]
+        eps = [torch.randn(1, 64, 3, generator=g).to(gpu_device) for _ in range(3)]
+        me, mg = copy.deepcopy(base), copy.deepcopy(base)
+        te = DPTrainer(me, lr=1e-3, clip_grads=1e-5, graph=True)
+        tg = DPTrainer(mg, lr=1e-3, clip_grads=1e-5, graph=True)
+        replay = tg.capture(xs[0], eps[0])
+        for x, e in zip(xs, eps):
+            le = [float(t.double().mean()) for t in te.step(x, e)]
+            lg = [float(t.double().mean()) for t in replay(x, e)]
+            torch.cuda.synchronize()
+            assert le == pytest.approx(lg, rel=1e-5)
+        pe = torch.cat([p.detach().flatten() for p in me.parameters()])
+        pg = torch.cat([p.detach().flatten() for p in mg.parameters()])
+        torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-6)
+        be = torch.cat([b.double().flatten() for b in me.buffers()])
+        bg = torch.cat([b.double().flatten() for b in mg.buffers()])
+        torch.testing.assert_close(bg, be, rtol=1e-4, atol=1e-6)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
