@@ -141,6 +141,18 @@ int lv_group_action_fwd(const float* ang, const float* F, int64_t F_batch_stride
  * over the batch (deterministic two-stage reduction through the workspace) when
  * F_batch_stride == 0, else (n,M,C).  Workspace bytes from the query below. */
 size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F);
+
+/* Launch plans (host only, no GPU call; for tests and capacity planning).  plan[] gets
+ * LV_PLAN_LEN values: [0] forward: tile kernel (1) or grid-stride kernel (0); backward:
+ * spectrum mode (0 per-sample, 1 shared in LDS, 2 shared from global memory with the dF
+ * slab in the workspace -- the large-tile fallback), [1] grid blocks,
+ * [2] degree segments, [3] threads per block, [4] dynamic LDS bytes per block,
+ * [5] samples per block group, [6] forward: write-through stores / backward: workspace
+ * bytes, [7..] segment boundaries seg_lo[0..segments] (then -1).  n > 0. */
+#define LV_PLAN_LEN 24
+int lv_action_fwd_plan(int fused, int64_t F_batch_stride, int out_dtype, int64_t n, int L, int C,
+                       int64_t* plan);
+int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* plan);
 int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride,
                         const float* gout, float* gang, float* gF, int64_t n, int L, int C,
                         int transpose, void* workspace, size_t ws_bytes, void* stream);

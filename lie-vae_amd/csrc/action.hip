@@ -187,37 +187,31 @@ int check_common(int64_t n, int L, int C, int dtype) {
   return LV_OK;
 }
 
-int action_fwd_common(bool fused, const float* ang, const float* mu, const float* v, const float* F,
-                      int64_t Fstride, void* out, int out_dtype, float* ang_out, int64_t n, int L,
-                      int C, int transpose, hipStream_t stream) {
-  clear_error();
+// Argument checks + launch plan of the forward (host only, no GPU call): the tile
+// kernel when its LDS footprint fits, else the grid-stride kernel (gx blocks of
+// kWavesPerBlock waves x gy degree segments).  n > 0.
+int check_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C) {
   if (int e = check_common(n, L, C, out_dtype)) return e;
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
   LV_CHECK_ARG(Fstride == 0 || Fstride == MC, "F batch stride must be 0 or M*C=%lld", (long long)MC);
-  if (n == 0) return LV_OK;
-  LV_CHECK_ARG(F && out, "null F/out");
-  LV_CHECK_ARG(fused ? (v != nullptr) : (ang != nullptr), "null input");
   LV_CHECK_ARG(!fused || Fstride == 0, "the fused path takes a shared spectrum (F batch stride 0)");
   LV_CHECK_ARG(Fstride == 0 || out_dtype == LV_DTYPE_F32, "bf16 output needs a shared spectrum");
-  FwdLaunch p{};
-  p.a.ang = ang;
-  p.a.mu = mu;
-  p.a.v = v;
-  p.a.F = F;
+  return LV_OK;
+}
+
+int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C, FwdLaunch& p) {
+  if (int e = check_fwd(fused, Fstride, out_dtype, n, L, C)) return e;
+  const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
+  p = FwdLaunch{};
   p.a.Fstride = Fstride;
-  p.a.out = out;
-  p.a.ang_out = ang_out;
   p.a.n = n;
   p.a.MC = MC;
   p.a.C = C;
   p.a.Sw = 64 / C;
-  p.a.transpose = transpose ? 1 : 0;
   p.fused = fused;
   p.dtype = out_dtype;
-  p.stream = stream;
   const int ob = out_dtype == LV_DTYPE_BF16 ? 2 : 4;
-  if (Fstride == 0 && plan_tile(p, L, ob))
-    return dispatch_L<FwdLauncher>(L, p);
+  if (Fstride == 0 && plan_tile(p, L, ob)) return LV_OK;
   const double P = fused ? kPrologueFused : kPrologueFwd;
   static const int kEnvFwdNseg = env_int("LV_FWD_NSEG", 0);  // A/B testing only
   const int nseg = kEnvFwdNseg > 0 ? std::min(kEnvFwdNseg, std::min(L + 1, kMaxSeg))
@@ -227,8 +221,35 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   LV_CHECK_ARG(gx <= 0x7fffffff, "batch too large");
   p.gx = (int)gx;
   p.gy = nseg;
-  p.fused = fused;
-  p.dtype = out_dtype;
+  // LDS: the widest segment's spectrum slice (shared F), then the per-sample trig tables
+  // from kTrigLdsMinL
+  int fmax = 0;
+  if (Fstride == 0)
+    for (int k = 0; k < nseg; ++k)
+      fmax = std::max(fmax, (fseg_rows(p.a.seg_lo[k], p.a.seg_lo[k + 1]) * C + 3) & ~3);
+  p.a.fpitch = fmax;
+  const size_t trig = L >= kTrigLdsMinL ? (size_t)kWavesPerBlock * p.a.Sw * trig_row_floats(L) : 0;
+  p.lds = sizeof(float) * ((size_t)fmax + trig);
+  return LV_OK;
+}
+
+int action_fwd_common(bool fused, const float* ang, const float* mu, const float* v, const float* F,
+                      int64_t Fstride, void* out, int out_dtype, float* ang_out, int64_t n, int L,
+                      int C, int transpose, hipStream_t stream) {
+  clear_error();
+  if (int e = check_fwd(fused, Fstride, out_dtype, n, L, C)) return e;
+  if (n == 0) return LV_OK;
+  LV_CHECK_ARG(F && out, "null F/out");
+  LV_CHECK_ARG(fused ? (v != nullptr) : (ang != nullptr), "null input");
+  FwdLaunch p;
+  if (int e = plan_fwd(fused, Fstride, out_dtype, n, L, C, p)) return e;
+  p.a.ang = ang;
+  p.a.mu = mu;
+  p.a.v = v;
+  p.a.F = F;
+  p.a.out = out;
+  p.a.ang_out = ang_out;
+  p.a.transpose = transpose ? 1 : 0;
   p.stream = stream;
   return dispatch_L<FwdLauncher>(L, p);
 }
@@ -253,41 +274,56 @@ constexpr int64_t kBwdMaxBlocks = 4096;
 // 40.8 / 32.0 / 42.6 / 39.1 / 44.8 / 45.5 us per call.
 constexpr double kBwdSegCost = 2.2 * 1000.0;
 
+// Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
+// high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
+// the block's workspace row (kBwdFSharedGlobal); per-sample spectra only need the bigger
+// LDS budget.  One block per CU at most, so fewer blocks (and workspace rows) suffice.
+constexpr size_t kBwdMaxLdsFallback = 160 * 1024;
+constexpr int64_t kBwdMaxBlocksFallback = 1024;
+
 struct BwdPlan {
-  int Sw, nseg, gx, fpitch;
+  int Sw, nseg, gx, fpitch, fmode;
   int64_t groups;
   int seg_lo[kMaxSeg + 1];
   size_t lds, ws;
 };
 
 bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
-  static const int kEnvNseg = env_int("LV_BWD_NSEG", 0);  // A/B testing only
+  static const int kEnvNseg = env_int("LV_BWD_NSEG", 0);      // A/B testing only
+  static const int kEnvGlobal = env_int("LV_BWD_FGLOBAL", 0);  // force the fallback (tests)
   b = BwdPlan{};
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, true);
-  for (int Sw = 64 / C; Sw >= 1; --Sw) {
-    const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
-    int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / kBwdSegCost)));
-    if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
-    nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
-    if (3 * Sw > 64 * nseg || nseg > 8) continue;
-    plan_segments(L, nseg, kTilePrologue, true, b.seg_lo);
-    int fp = 0;
-    if (sharedF)
-      for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(b.seg_lo[k], b.seg_lo[k + 1]) * C);
-    b.fpitch = (fp + 3) & ~3;
-    const size_t lds = (size_t)tile_stage_bytes(Sw, MC, 4) +
-                       sizeof(float) * ((size_t)bwd_trig_floats(Sw, L) + (size_t)nseg * 64 * 3 +
-                                        (sharedF ? (size_t)MC : 0) + (size_t)nseg * b.fpitch);
-    if (lds > kBwdMaxLds) continue;
-    b.Sw = Sw;
-    b.nseg = nseg;
-    b.groups = groups;
-    b.gx = (int)std::min<int64_t>(groups, kBwdMaxBlocks);
-    b.lds = lds;
-    b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)MC : 0;
-    return true;
+  for (int fallback = (kEnvGlobal && sharedF) ? 1 : 0; fallback < 2; ++fallback) {
+    const int fmode = !sharedF ? kBwdFSample : (fallback ? kBwdFSharedGlobal : kBwdFShared);
+    const size_t cap = fallback ? kBwdMaxLdsFallback : kBwdMaxLds;
+    for (int Sw = 64 / C; Sw >= 1; --Sw) {
+      const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
+      int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / kBwdSegCost)));
+      if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
+      nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
+      if (3 * Sw > 64 * nseg || nseg > 8) continue;
+      plan_segments(L, nseg, kTilePrologue, true, b.seg_lo);
+      int fp = 0;
+      if (fmode == kBwdFShared)
+        for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(b.seg_lo[k], b.seg_lo[k + 1]) * C);
+      b.fpitch = (fp + 3) & ~3;
+      const size_t lds = (size_t)tile_stage_bytes(Sw, MC, 4) +
+                         sizeof(float) * ((size_t)bwd_trig_floats(Sw, L) + (size_t)nseg * 64 * 3 +
+                                          (fmode == kBwdFShared ? (size_t)MC : 0) +
+                                          (size_t)nseg * b.fpitch);
+      if (lds > cap) continue;
+      b.Sw = Sw;
+      b.nseg = nseg;
+      b.fmode = fmode;
+      b.groups = groups;
+      b.gx = (int)std::min<int64_t>(groups, fallback ? kBwdMaxBlocksFallback : kBwdMaxBlocks);
+      if (kEnvGlobal && sharedF) b.gx = (int)std::min<int64_t>(groups, kBwdMaxBlocks);
+      b.lds = lds;
+      b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)MC : 0;
+      return true;
+    }
   }
   return false;
 }
@@ -296,6 +332,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
 }  // namespace lv
 
 using namespace lv;
+static_assert(7 + kMaxSeg + 1 == LV_PLAN_LEN, "plan layout (include/lievae.h)");
 
 extern "C" {
 
@@ -369,6 +406,7 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
   p.gx = b.gx;
   p.nseg = b.nseg;
+  p.fmode = b.fmode;
   p.lds = b.lds;
   p.stream = st;
   if (int e = kBwdRun[L](p)) return e;
@@ -376,6 +414,42 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
   hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, 64)), dim3(64 * kBwdReduceWaves),
                      0, st, (const float*)workspace, gF, MC, b.gx);
   LV_RETURN_LAUNCH("action_bwd_reduce_kernel");
+}
+
+int lv_action_fwd_plan(int fused, int64_t F_batch_stride, int out_dtype, int64_t n, int L, int C,
+                       int64_t* plan) {
+  clear_error();
+  LV_CHECK_ARG(plan, "null plan");
+  LV_CHECK_ARG(n > 0, "n must be > 0 (got %lld)", (long long)n);
+  FwdLaunch p;
+  if (int e = plan_fwd(fused != 0, F_batch_stride, out_dtype, n, L, C, p)) return e;
+  plan[0] = p.tile ? 1 : 0;
+  plan[1] = p.gx;
+  plan[2] = p.gy;
+  plan[3] = p.tile ? 64 * p.gy : kThreads;
+  plan[4] = (int64_t)p.lds;
+  plan[5] = p.a.Sw;
+  plan[6] = p.a.write_through;
+  for (int k = 0; k <= kMaxSeg; ++k) plan[7 + k] = k <= p.gy ? p.a.seg_lo[k] : -1;
+  return LV_OK;
+}
+
+int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* plan) {
+  clear_error();
+  LV_CHECK_ARG(plan, "null plan");
+  LV_CHECK_ARG(n > 0, "n must be > 0 (got %lld)", (long long)n);
+  if (int e = check_common(n, L, C, LV_DTYPE_F32)) return e;
+  BwdPlan b;
+  LV_CHECK_ARG(plan_bwd(n, L, C, shared_F != 0, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
+  plan[0] = b.fmode;
+  plan[1] = b.gx;
+  plan[2] = b.nseg;
+  plan[3] = 64 * b.nseg;
+  plan[4] = (int64_t)b.lds;
+  plan[5] = b.Sw;
+  plan[6] = (int64_t)b.ws;
+  for (int k = 0; k <= kMaxSeg; ++k) plan[7 + k] = k <= b.nseg ? b.seg_lo[k] : -1;
+  return LV_OK;
 }
 
 int lv_wigner_d_fwd(const float* ang, float* D, int64_t n, int L, void* stream) {

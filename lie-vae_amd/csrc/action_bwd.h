@@ -25,6 +25,12 @@ namespace lv {
 // blocks loop over groups (grid capped so the workspace stays
 // bounded), write their slab to the workspace once, and action_bwd_reduce_kernel sums
 // the slabs in block order.  No atomics: bitwise reproducible.
+// FM (spectrum mode): kBwdFSample per-sample spectrum, kBwdFShared shared spectrum with
+// its slices and the dF slab in LDS, kBwdFSharedGlobal shared spectrum read from global
+// memory and the slab accumulated in place in the block's workspace row -- the fallback
+// for tiles too large to leave room for both (large C at high l); same summation order,
+// so bitwise equal to kBwdFShared for the same plan.
+constexpr int kBwdFSample = 0, kBwdFShared = 1, kBwdFSharedGlobal = 2;
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
@@ -115,8 +121,10 @@ __device__ __forceinline__ float xm_dd(const Mult<l>& m, const float (&g)[2 * l 
 // tile_flush; the LDS tile starts `mis` bytes past a 16-B boundary.
 constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per thread
 
-template <int LT, int CT, bool SHAREDF>
+template <int LT, int CT, int FM>
 __global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
+  constexpr bool SHAREDF = FM != kBwdFSample;
+  constexpr bool GSLAB = FM == kBwdFSharedGlobal;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int kRow = TrigLds<LT>::kRow;
@@ -135,13 +143,16 @@ __global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
   // LDS: [gout / dF tile][multiples table][angle partials][dF slab (shared F)][F slices]
   float* trig = lds + (stage_bytes >> 2);
   float* apart = trig + bwd_trig_floats(Sw, LT);               // [nseg][64][3]
-  float* slabL = apart + (nthr >> 6) * 64 * 3;                 // [M*C] (shared F)
-  float* Fw = slabL + (SHAREDF ? (int)MC : 0) + wave * a.fpitch;
+  // dF slab: LDS [M*C] (kBwdFShared), or this block's workspace row (kBwdFSharedGlobal)
+  float* slabL = GSLAB ? a.ws_F + (int64_t)blockIdx.x * MC : apart + (nthr >> 6) * 64 * 3;
+  float* Fw = apart + (nthr >> 6) * 64 * 3 + (FM == kBwdFShared ? (int)MC : 0) + wave * a.fpitch;
   // spectrum slice (shared F): once per block
   constexpr int kFPer = 6;
   const int fcnt = SHAREDF ? (hi * hi - rows_lo) * C : 0;
   const float* fsrc = a.F + rows_lo * C;
-  if constexpr (SHAREDF) {
+  if constexpr (GSLAB) {
+    for (int e = lane; e < fcnt; e += 64) slabL[rows_lo * C + e] = 0.f;  // this wave's rows
+  } else if constexpr (SHAREDF) {
     float fv[kFPer];
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
@@ -171,8 +182,8 @@ __global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
       }
     }
   }
-  const float* Fl = CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo;
-  const int fstep = CT > 0 ? C : 1;
+  const float* Fl = GSLAB ? a.F + c : (CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo);
+  const int fstep = (GSLAB || CT > 0) ? C : 1;
   const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
 
@@ -315,7 +326,7 @@ __global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
       tile_flush<float, 1>(a.gF + s0 * MC, stage_b, mis, nbytes, tid, nthr);
     block_sync_lds();  // the next group overwrites the tile, the table and the partials
   }
-  if constexpr (SHAREDF) {
+  if constexpr (FM == kBwdFShared) {
     float* slab = a.ws_F + (int64_t)blockIdx.x * MC;
     for (int e = lane; e < fcnt; e += 64) slab[rows_lo * C + e] = slabL[rows_lo * C + e];
   }
@@ -326,7 +337,7 @@ constexpr int kBwdReduceWaves = 16;
 
 struct BwdLaunch {
   ActionBwdArgs a;
-  int gx, nseg;
+  int gx, nseg, fmode;
   size_t lds;
   hipStream_t stream;
 };
@@ -338,12 +349,14 @@ struct BwdLauncher {
 template <int LT>
 int BwdLauncher<LT>::run(BwdLaunch& p) {
   const dim3 grid(p.gx), block(64 * p.nseg);
-  if (p.a.Fstride != 0)
-    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, false>), grid, block, p.lds, p.stream, p.a);
+  if (p.fmode == kBwdFSample)
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSample>), grid, block, p.lds, p.stream, p.a);
+  else if (p.fmode == kBwdFSharedGlobal)
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSharedGlobal>), grid, block, p.lds, p.stream, p.a);
   else if (p.a.C == kTileFastC)
-    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, true>), grid, block, p.lds, p.stream, p.a);
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared>), grid, block, p.lds, p.stream, p.a);
   else
-    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, true>), grid, block, p.lds, p.stream, p.a);
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFShared>), grid, block, p.lds, p.stream, p.a);
   LV_RETURN_LAUNCH("action_bwd_tile_kernel");
 }
 

@@ -77,6 +77,10 @@ struct TrigLds {
   static constexpr int TP = (LT + 1 + 3) & ~3;
   static constexpr int kRow = 6 * TP + 4;
 };
+// Run-time twin of TrigLds<L>::kRow (host launch planning).
+__host__ __device__ constexpr int trig_row_floats(int L) { return 6 * ((L + 1 + 3) & ~3) + 4; }
+static_assert(trig_row_floats(10) == TrigLds<10>::kRow && trig_row_floats(20) == TrigLds<20>::kRow,
+              "trig row layout");
 
 // Write slot q's multiples f = 0..upto (trig_fill's recurrence, same rounding).
 template <int LT>

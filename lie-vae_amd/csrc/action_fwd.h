@@ -445,14 +445,8 @@ int FwdLauncher<LT>::run(FwdLaunch& p) {
       launch_tile<0>(p, bf16);
     LV_RETURN_LAUNCH("action_fwd_tile_kernel");
   }
-  int fmax = 0;
   const bool shared = p.a.Fstride == 0;
-  if (shared)
-    for (int k = 0; k < p.gy; ++k)
-      fmax = max(fmax, (fseg_rows(p.a.seg_lo[k], p.a.seg_lo[k + 1]) * p.a.C + 3) & ~3);
-  p.a.fpitch = fmax;  // trig tables follow the spectrum slice (LT >= kTrigLdsMinL)
-  const size_t trig = LT >= kTrigLdsMinL ? (size_t)kWavesPerBlock * p.a.Sw * TrigLds<LT>::kRow : 0;
-  const size_t lds = sizeof(float) * ((size_t)fmax + trig);
+  const size_t lds = p.lds;  // spectrum slice + trig tables (plan_fwd in action.hip)
   const dim3 grid(p.gx, p.gy), block(kThreads);
   if (p.fused) {  // the fused path takes a shared spectrum (ActionNet's item_rep)
     if (bf16)

@@ -42,6 +42,8 @@ _SIGS = {
     "lv_s2s2_fwd_f64": [_P, _P, _P, _I64, _P],
     "lv_s2s2_bwd_f64": [_P, _P, _P, _P, _P, _I64, _P],
     "lv_wigner_d_fwd": [_P, _P, _I64, _I, _P],
+    "lv_action_fwd_plan": [_I, _I64, _I, _I64, _I, _I, _P],
+    "lv_group_action_bwd_plan": [_I64, _I, _I, _I, _P],
     "lv_group_action_fwd": [_P, _P, _I64, _P, _I, _I64, _I, _I, _I, _P],
     "lv_group_action_bwd": [_P, _P, _I64, _P, _P, _P, _I64, _I, _I, _I, _P, _SZ, _P],
     "lv_exp_eazyz_vjp": [_P, _P, _P, _P, _P, _I64, _P],
@@ -100,6 +102,20 @@ def call(name, *args):
     rc = getattr(load(), name)(*args)
     if rc != 0:
         raise LieVaeHipError(f"{name} failed ({rc}): {last_error()}")
+
+
+PLAN_LEN = 24  # LV_PLAN_LEN
+PLAN_FIELDS = ("tile", "blocks", "segments", "threads", "lds_bytes", "samples_per_group", "aux")
+
+
+def plan(kind, *args):
+    """Host-only launch plan ("fwd": fused, F_batch_stride, out_dtype, n, L, C;
+    "bwd": n, L, C, shared_F) as a dict; no GPU call (include/lievae.h LV_PLAN_LEN)."""
+    buf = (ctypes.c_int64 * PLAN_LEN)()
+    call("lv_action_fwd_plan" if kind == "fwd" else "lv_group_action_bwd_plan", *args, buf)
+    d = dict(zip(PLAN_FIELDS, buf[:7]))
+    d["seg_lo"] = [x for x in buf[7:] if x >= 0]
+    return d
 
 
 def stream():

@@ -338,6 +338,72 @@ def test_action_bwd_reproducible_and_looped(gpu_device):
     assert_normwise(host(f.grad)[None], gf_sum.cpu().numpy()[None], 1e-5, what="looped dF")
 
 
+def test_action_large_tiles_fallback_vs_oracle(gpu_device):
+    """Tiles too large for the LDS plans (large C at high l; include/lievae.h plan mode 2):
+    the forward's grid-stride kernel and the backward's global-spectrum fallback (dF slab
+    in the workspace), and a per-sample spectrum at l = 20, C = 64 (LDS budget raised),
+    against the oracle's autograd."""
+    import lie_vae._lib as lib
+    import lie_vae._ops as ops
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(12)
+    for L, C, n, shared in [(20, 16, 97, True), (15, 64, 61, True), (20, 64, 13, False)]:
+        mode = lib.plan("bwd", n, L, C, int(shared))["tile"]
+        assert mode == (2 if shared else 0), (L, C, mode)
+        M = (L + 1) ** 2
+        ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n))
+        F = torch.randn(M, C, generator=gen) if shared else torch.randn(n, M, C, generator=gen)
+        gout = torch.randn(n, M, C, generator=gen)
+        a = ang.to(gpu_device).requires_grad_(True)
+        f = F.to(gpu_device).requires_grad_(True)
+        y = ops.group_action(a, f, L)
+        (y * gout.to(gpu_device)).sum().backward()
+        a64 = ang.double().requires_grad_(True)
+        f64 = F.double().requires_grad_(True)
+        fe = f64.expand(n, -1, -1) if shared else f64
+        y64 = lie_ref.block_wigner_apply(a64, fe, L)
+        (y64 * gout.double()).sum().backward()
+        assert_normwise(host(y).reshape(n, -1), y64.detach().numpy().reshape(n, -1), 1e-5,
+                        what=f"y L={L} C={C}")
+        assert_normwise(host(a.grad), a64.grad.numpy(), 1e-4, what=f"gang L={L} C={C}")
+        assert_normwise(host(f.grad).reshape(-1, M * C), f64.grad.numpy().reshape(-1, M * C),
+                        1e-4, what=f"gF L={L} C={C}")
+
+
+_FGLOBAL_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import lie_vae._ops as ops
+L, n = 10, 4099
+g = torch.Generator().manual_seed(13)
+ang = (torch.rand(n, 3, generator=g) * 6 - 3).cuda().requires_grad_(True)
+F = torch.randn((L + 1) ** 2, 10, generator=g).cuda().requires_grad_(True)
+gout = torch.randn(n, (L + 1) ** 2, 10, generator=g).cuda()
+(ops.group_action(ang, F, L) * gout).sum().backward()
+np.savez(sys.argv[2], ga=ang.grad.cpu().numpy(), gf=F.grad.cpu().numpy())
+"""
+
+
+def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
+    """The fallback mode (spectrum from global memory, dF slab accumulated in the block's
+    workspace row) keeps the LDS mode's summation order: forced on for the config-2 shape
+    (LV_BWD_FGLOBAL=1, read once per process, hence a child process), the gradients are
+    bitwise those of the LDS mode."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "lie-vae_amd")
+    outs = []
+    for forced in ("0", "1"):
+        path = str(tmp_path / f"g{forced}.npz")
+        env = dict(os.environ, LV_BWD_FGLOBAL=forced)
+        subprocess.run([sys.executable, "-c", _FGLOBAL_SCRIPT, pkg, path], env=env, check=True,
+                       timeout=180)
+        outs.append(np.load(path))
+    assert np.array_equal(outs[0]["ga"], outs[1]["ga"])
+    assert np.array_equal(outs[0]["gf"], outs[1]["gf"])
+
+
 def test_exp_eazyz_vjp_matches_modular_bitwise(gpu_device):
     """lv_exp_eazyz_vjp (the fused path's prologue backward in one kernel) against the
     three modular kernels it replaces -- so3_exp_fwd / so3_sample_fwd, mat_to_eazyz_bwd,

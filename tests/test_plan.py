@@ -1,0 +1,102 @@
+"""Host launch planning of the group-action kernels (action.hip plan_fwd / plan_bwd),
+through the host-only C-ABI entries lv_action_fwd_plan / lv_group_action_bwd_plan: no
+GPU call, so this runs on CPU.  The invariants are what the kernels assume about their
+grid and LDS (action_fwd.h, action_bwd.h); a plan that broke one would fault the GPU."""
+import pytest
+
+from lie_vae import _lib
+
+LDS_PER_CU = 160 * 1024
+TILE_MAX_LDS = 80 * 1024       # action.hip kTileMaxLds
+BWD_MAX_LDS = 96 * 1024        # action.hip kBwdMaxLds
+BWD_MAX_BLOCKS = 4096          # action.hip kBwdMaxBlocks
+F32, BF16 = _lib.LV_DTYPE_F32, _lib.LV_DTYPE_BF16
+NS = (1, 5, 6, 7, 683, 4096, 8192, 65536, 1 << 20)
+
+
+def _check_segments(p, L):
+    seg = p["seg_lo"]
+    assert len(seg) == p["segments"] + 1
+    assert seg[0] == 0 and seg[-1] == L + 1
+    assert all(a < b for a, b in zip(seg, seg[1:])), seg
+
+
+@pytest.mark.parametrize("L", list(range(0, 21)))
+def test_forward_plans_fit_the_kernels(L):
+    for C in (1, 3, 10, 16, 64):
+        M = (L + 1) ** 2
+        for n in NS:
+            for fused, fstride, dt in ((1, 0, F32), (1, 0, BF16), (0, 0, F32), (0, 0, BF16),
+                                       (0, M * C, F32)):
+                p = _lib.plan("fwd", fused, fstride, dt, n, L, C)
+                _check_segments(p, L)
+                assert p["samples_per_group"] == 64 // C
+                assert p["lds_bytes"] <= LDS_PER_CU
+                assert p["threads"] <= 1024 and p["threads"] % 64 == 0
+                if p["tile"]:
+                    assert fstride == 0
+                    # __launch_bounds__(512); the prologue needs 3 threads per sample
+                    assert p["threads"] == 64 * p["segments"] <= 512
+                    assert 3 * p["samples_per_group"] <= p["threads"]
+                    assert p["lds_bytes"] <= TILE_MAX_LDS
+                    assert p["blocks"] * p["samples_per_group"] >= n
+                    assert (p["blocks"] - 1) * p["samples_per_group"] < n
+                else:
+                    waves = p["threads"] // 64
+                    assert p["blocks"] * waves * p["samples_per_group"] >= n
+                    assert p["segments"] <= 16
+
+
+@pytest.mark.parametrize("L", list(range(0, 21)))
+def test_backward_plans_fit_the_kernels(L):
+    for C in (1, 3, 10, 16, 64):
+        MC = (L + 1) ** 2 * C
+        for n in NS:
+            for shared in (1, 0):
+                p = _lib.plan("bwd", n, L, C, shared)
+                _check_segments(p, L)
+                assert p["threads"] == 64 * p["segments"] <= 512
+                assert 3 * p["samples_per_group"] <= p["threads"]
+                assert 1 <= p["samples_per_group"] <= 64 // C
+                mode = p["tile"]  # backward: spectrum mode
+                assert mode == (0 if not shared else mode) and mode in ((1, 2) if shared else (0,))
+                fallback = mode == 2 or p["lds_bytes"] > BWD_MAX_LDS
+                assert p["lds_bytes"] <= (LDS_PER_CU if fallback else BWD_MAX_LDS)
+                groups = -(-n // p["samples_per_group"])
+                assert p["blocks"] == min(groups, 1024 if fallback else BWD_MAX_BLOCKS)
+                assert p["aux"] == (4 * p["blocks"] * MC if shared else 0)
+                assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
+
+
+def test_pinned_plans_of_the_benchmark_configs():
+    # config 2 (bench.py): 683 blocks of 6 samples, spectrum in the tile's last slot
+    # (6*1210*4 + 16 tile + 6*76*4 trig = 30,880 B -> 5 blocks per CU), write-through
+    p = _lib.plan("fwd", 1, 0, F32, 4096, 10, 10)
+    assert (p["tile"], p["blocks"], p["lds_bytes"], p["aux"]) == (1, 683, 30880, 1)
+    assert _lib.plan("fwd", 1, 0, F32, 65536, 10, 10)["aux"] == 0  # > 24 MB: nt stores
+    # config 5: bf16 tile (6*4410*2 + 16, rounded to 16 B) + separate fp32 spectrum copy + trig
+    p = _lib.plan("fwd", 1, 0, BF16, 8192, 20, 10)
+    assert (p["tile"], p["blocks"], p["lds_bytes"]) == (1, 1366, 52944 + 17640 + 3552)
+    # backward at the config-2 size: 2 segments (profiles/r02_bwd_nseg_sweep.txt)
+    b = _lib.plan("bwd", 4096, 10, 10, 1)
+    assert (b["tile"], b["segments"], b["blocks"], b["samples_per_group"]) == (1, 2, 683, 6)
+    # every (l, C) has a backward plan; large tiles take the global-spectrum fallback
+    assert _lib.plan("bwd", 4096, 20, 64, 1)["tile"] == 2
+    assert _lib.plan("bwd", 4096, 20, 13, 1)["tile"] == 1
+
+
+@pytest.mark.parametrize("args", [
+    ("fwd", 1, 0, F32, 16, 21, 10),           # l_max > 20
+    ("fwd", 1, 0, F32, 16, 10, 0),            # C < 1
+    ("fwd", 1, 0, F32, 16, 10, 65),           # C > 64
+    ("fwd", 1, 1210, F32, 16, 10, 10),        # fused path: shared spectrum only
+    ("fwd", 0, 1210, BF16, 16, 10, 10),       # bf16 out needs a shared spectrum
+    ("fwd", 0, 7, F32, 16, 10, 10),           # bad batch stride
+    ("fwd", 1, 0, 5, 16, 10, 10),             # bad dtype
+    ("fwd", 1, 0, F32, 0, 10, 10),            # n = 0 has no plan
+    ("bwd", 16, 21, 10, 1),
+    ("bwd", 0, 10, 10, 1),
+])
+def test_plan_rejects_bad_arguments(args):
+    with pytest.raises(_lib.LieVaeHipError):
+        _lib.plan(*args)
