@@ -219,6 +219,21 @@ class DPTrainer:
             ts += [t for t in self.opt.state.get(p, {}).values() if torch.is_tensor(t)]
         return ts
 
+    def _drop_autograd_refs(self):
+        """The model keeps its last sample (VAE.z, the latent modules' z / v / sigma) with
+        the autograd graph attached; that graph holds the parameters' AccumulateGrad nodes,
+        which would then keep the eager stream and break capture on the side stream."""
+        def strip(v):
+            if torch.is_tensor(v) and v.grad_fn is not None:
+                return v.detach()
+            if isinstance(v, (list, tuple)):
+                return type(v)(strip(u) for u in v)
+            return v
+        for m in self.model.modules():
+            for k, v in list(vars(m).items()):
+                if not k.startswith("_"):
+                    setattr(m, k, strip(v))
+
     def capture(self, x, eps=None, warmup=3):
         """Record one training step as a hipGraph; returns ``replay(x=None, eps=None)``
         which copies new inputs into the graph's static buffers, replays the step and
@@ -237,6 +252,7 @@ class DPTrainer:
             raise ValueError("capture() cannot run the per-step NaN check")
         beta = self.beta_schedule.value
         dev = x.device
+        self._drop_autograd_refs()
         gx = x.detach().clone()
         geps = None if eps is None else eps.detach().clone()
         had_state = {p for p in self.model.parameters() if self.opt.state.get(p)}

@@ -352,13 +352,16 @@ def test_dp_trainer_graph_replay_matches_eager(gpu_device):
                    rgb=True, batch_norm=True, deconv_hidden=200,
                    mean_mode="s2s2").to(gpu_device)
         g = torch.Generator().manual_seed(4)
-        xs = [torch.rand(64, 3, 64, 64, generator=g).to(gpu_device) for _ in range(3)]
-        eps = [torch.randn(1, 64, 3, generator=g).to(gpu_device) for _ in range(3)]
+        xs = [torch.rand(64, 3, 64, 64, generator=g).to(gpu_device) for _ in range(4)]
+        eps = [torch.randn(1, 64, 3, generator=g).to(gpu_device) for _ in range(4)]
         me, mg = copy.deepcopy(base), copy.deepcopy(base)
         te = DPTrainer(me, lr=1e-3, clip_grads=1e-5, graph=True)
         tg = DPTrainer(mg, lr=1e-3, clip_grads=1e-5, graph=True)
-        replay = tg.capture(xs[0], eps[0])
-        for x, e in zip(xs, eps):
+        # one eager step first (Adam state exists, the model holds a live autograd graph)
+        te.step(xs[0], eps[0])
+        tg.step(xs[0], eps[0])
+        replay = tg.capture(xs[1], eps[1])
+        for x, e in zip(xs[1:], eps[1:]):
             le = [float(t.double().mean()) for t in te.step(x, e)]
             lg = [float(t.double().mean()) for t in replay(x, e)]
             torch.cuda.synchronize()
