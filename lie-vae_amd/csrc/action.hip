@@ -334,6 +334,61 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
 using namespace lv;
 static_assert(7 + kMaxSeg + 1 == LV_PLAN_LEN, "plan layout (include/lievae.h)");
 
+namespace {
+int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
+                      const float* gout, float* gang, float* gF, const float* mu, const float* v,
+                      float* gmu, float* gv, int64_t n, int L, int C, int transpose,
+                      void* workspace, size_t ws_bytes, void* stream) {
+  if (int e = check_common(n, L, C, LV_DTYPE_F32)) return e;
+  const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
+  LV_CHECK_ARG(F_batch_stride == 0 || F_batch_stride == MC, "F batch stride must be 0 or M*C");
+  const bool sharedF = F_batch_stride == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    if (sharedF && gF) (void)hipMemsetAsync(gF, 0, sizeof(float) * MC, st);
+    return LV_OK;
+  }
+  LV_CHECK_ARG(ang && F && gout && gF && (gang || v), "null pointer argument");
+  LV_CHECK_ARG(!v || (gv && (!mu || gmu)), "null VJP output");
+  BwdPlan b;
+  LV_CHECK_ARG(plan_bwd(n, L, C, sharedF, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
+  if (sharedF && (ws_bytes < b.ws || !workspace)) {
+    set_error("workspace too small: need %zu bytes", b.ws);
+    return LV_ERR_WORKSPACE;
+  }
+  BwdLaunch p{};
+  p.a.ang = ang;
+  p.a.F = F;
+  p.a.Fstride = F_batch_stride;
+  p.a.gout = gout;
+  p.a.gang = gang;
+  p.a.v = v;
+  p.a.mu = mu;
+  p.a.gv = gv;
+  p.a.gmu = gmu;
+  p.a.gF = gF;
+  p.a.ws_F = (float*)workspace;
+  p.a.n = n;
+  p.a.MC = MC;
+  p.a.groups = b.groups;
+  p.a.C = C;
+  p.a.Sw = b.Sw;
+  p.a.transpose = transpose ? 1 : 0;
+  p.a.fpitch = b.fpitch;
+  for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
+  p.gx = b.gx;
+  p.nseg = b.nseg;
+  p.fmode = b.fmode;
+  p.lds = b.lds;
+  p.stream = st;
+  if (int e = kBwdRun[L](p)) return e;
+  if (!sharedF) return LV_OK;
+  hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, 64)), dim3(64 * kBwdReduceWaves),
+                     0, st, (const float*)workspace, gF, MC, b.gx);
+  LV_RETURN_LAUNCH("action_bwd_reduce_kernel");
+}
+}  // namespace
+
 extern "C" {
 
 int lv_group_action_fwd(const float* ang, const float* F, int64_t F_batch_stride, void* out,
@@ -368,52 +423,23 @@ size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F) {
   return b.ws;
 }
 
+
 int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride,
                         const float* gout, float* gang, float* gF, int64_t n, int L, int C,
                         int transpose, void* workspace, size_t ws_bytes, void* stream) {
   clear_error();
-  if (int e = check_common(n, L, C, LV_DTYPE_F32)) return e;
-  const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
-  LV_CHECK_ARG(F_batch_stride == 0 || F_batch_stride == MC, "F batch stride must be 0 or M*C");
-  const bool sharedF = F_batch_stride == 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (n == 0) {
-    if (sharedF && gF) (void)hipMemsetAsync(gF, 0, sizeof(float) * MC, st);
-    return LV_OK;
-  }
-  LV_CHECK_ARG(ang && F && gout && gang && gF, "null pointer argument");
-  BwdPlan b;
-  LV_CHECK_ARG(plan_bwd(n, L, C, sharedF, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
-  if (sharedF && (ws_bytes < b.ws || !workspace)) {
-    set_error("workspace too small: need %zu bytes", b.ws);
-    return LV_ERR_WORKSPACE;
-  }
-  BwdLaunch p{};
-  p.a.ang = ang;
-  p.a.F = F;
-  p.a.Fstride = F_batch_stride;
-  p.a.gout = gout;
-  p.a.gang = gang;
-  p.a.gF = gF;
-  p.a.ws_F = (float*)workspace;
-  p.a.n = n;
-  p.a.MC = MC;
-  p.a.groups = b.groups;
-  p.a.C = C;
-  p.a.Sw = b.Sw;
-  p.a.transpose = transpose ? 1 : 0;
-  p.a.fpitch = b.fpitch;
-  for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
-  p.gx = b.gx;
-  p.nseg = b.nseg;
-  p.fmode = b.fmode;
-  p.lds = b.lds;
-  p.stream = st;
-  if (int e = kBwdRun[L](p)) return e;
-  if (!sharedF) return LV_OK;
-  hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, 64)), dim3(64 * kBwdReduceWaves),
-                     0, st, (const float*)workspace, gF, MC, b.gx);
-  LV_RETURN_LAUNCH("action_bwd_reduce_kernel");
+  LV_CHECK_ARG(gang, "null gang");
+  return action_bwd_common(ang, F, F_batch_stride, gout, gang, gF, nullptr, nullptr, nullptr,
+                           nullptr, n, L, C, transpose, workspace, ws_bytes, stream);
+}
+
+int lv_fused_exp_action_bwd(const float* mu, const float* v, const float* ang, const float* F,
+                            const float* gout, float* gmu, float* gv, float* gF, int64_t n, int L,
+                            int C, int transpose, void* workspace, size_t ws_bytes, void* stream) {
+  clear_error();
+  if (n > 0) LV_CHECK_ARG(v && gv && (!mu || gmu), "null v / gv / gmu");
+  return action_bwd_common(ang, F, 0, gout, nullptr, gF, mu, v, gmu, gv, n, L, C, transpose,
+                           workspace, ws_bytes, stream);
 }
 
 int lv_action_fwd_plan(int fused, int64_t F_batch_stride, int out_dtype, int64_t n, int L, int C,

@@ -36,7 +36,11 @@ struct ActionBwdArgs {
   const float* F;
   int64_t Fstride;
   const float* gout;
-  float* gang;
+  float* gang;         // may be null when v is set (fused: the angle gradient stays in LDS)
+  const float* v;      // fused exp -> ZYZ VJP in the tail (lv_fused_exp_action_bwd), or null
+  const float* mu;     // (n,3,3) or null
+  float* gv;
+  float* gmu;
   float* gF;           // per-sample spectrum: written directly
   float* ws_F;         // [gridDim.x][M*C] (shared F only)
   int64_t n;
@@ -320,7 +324,28 @@ __global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
         for (int cc2 = 0; cc2 < C; ++cc2) sw += apart[(w * 64 + js * C + cc2) * 3 + i];
         r += sw;
       }
-      a.gang[(s0 + js) * 3 + i] = r;
+      if (a.gang) a.gang[(s0 + js) * 3 + i] = r;
+      if (a.v) trig[js * 3 + i] = r;  // the chains are done: the table is free
+    }
+    if (a.v) {  // fused path: exp -> ZYZ VJP of the group's samples (exp_eazyz_vjp_sample)
+      block_sync_lds();
+      if (tid < Sv) {
+        const int64_t s = s0 + tid;
+        float av[3], g[3], m[9], gm[9], o[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { av[k] = a.v[s * 3 + k]; g[k] = trig[tid * 3 + k]; }
+        if (a.mu) {
+#pragma unroll
+          for (int k = 0; k < 9; ++k) m[k] = a.mu[s * 9 + k];
+        }
+        exp_eazyz_vjp_sample(av, a.mu ? m : nullptr, g, gm, o);
+        if (a.mu) {
+#pragma unroll
+          for (int k = 0; k < 9; ++k) a.gmu[s * 9 + k] = gm[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a.gv[s * 3 + k] = o[k];
+      }
     }
     if constexpr (!SHAREDF)
       tile_flush<float, 1>(a.gF + s0 * MC, stage_b, mis, nbytes, tid, nthr);

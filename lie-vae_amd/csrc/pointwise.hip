@@ -114,32 +114,12 @@ template <typename T>
 __global__ void exp_eazyz_vjp_k(const T* mu, const T* v, const T* ga, T* gmu,
                                 T* gv, int64_t n) {
   LV_FOR_EACH(i, n) {
-    T a[3], r[9], z[9], q[4], g[3], gq[4], gz[9], o[3];
+    T a[3], g[3], m[9], gm[9], o[3];
     ld(v + i * 3, a);
     ld(ga + i * 3, g);
-    rodrigues_fwd(a, r);
-    T m[9];
-    if (mu) {
-      ld(mu + i * 9, m);
-      matmul3(m, r, z);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) z[k] = r[k];
-    }
-    mat_to_quat_fwd(z, q, nullptr);
-    quat_to_eazyz_bwd(q, g, gq);
-    mat_to_quat_bwd(z, gq, gz);
-    if (mu) {
-      T t[9], gr[9], acc[9];
-      matmul3_nt(gz, r, t);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc[k] = T(0) + t[k];
-      st(gmu + i * 9, acc);
-      matmul3_tn(m, gz, gr);
-      rodrigues_bwd(a, gr, o);
-    } else {
-      rodrigues_bwd(a, gz, o);
-    }
+    if (mu) ld(mu + i * 9, m);
+    exp_eazyz_vjp_sample(a, mu ? m : nullptr, g, gm, o);
+    if (mu) st(gmu + i * 9, gm);
     st(gv + i * 3, o);
   }
 }

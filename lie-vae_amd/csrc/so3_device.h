@@ -287,6 +287,39 @@ __device__ __forceinline__ void quat_to_mat_bwd(const T q0[4], const T g[9], T g
   gq[3] = (gn[3] - dot * w) / nrm;
 }
 
+// ------------------------------------------------- exp -> ZYZ vector-Jacobian product
+// The autograd backward of z = mu @ rodrigues(v) (or z = rodrigues(v)) followed by
+// group_matrix_to_eazyz (reparameterize.py:269-273, lie_tools.py:56-64,112-180): g = dL/d
+// angles -> gm = dL/dmu (when m != nullptr), gv = dL/dv, in the same operation order as
+// the modular kernels lv_so3_exp_fwd + lv_mat_to_eazyz_bwd + lv_so3_exp_bwd (or the
+// so3_sample pair), hence bitwise equal to them.  Shared by lv_exp_eazyz_vjp and the
+// fused backward tile kernel's tail.
+template <typename T>
+__device__ __forceinline__ void exp_eazyz_vjp_sample(const T a[3], const T* m, const T g[3],
+                                                     T gm[9], T gv[3]) {
+  T r[9], z[9], q[4], gq[4], gz[9];
+  rodrigues_fwd(a, r);
+  if (m) {
+    matmul3(m, r, z);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) z[k] = r[k];
+  }
+  mat_to_quat_fwd(z, q, nullptr);
+  quat_to_eazyz_bwd(q, g, gq);
+  mat_to_quat_bwd(z, gq, gz);
+  if (m) {
+    T t[9], gr[9];
+    matmul3_nt(gz, r, t);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) gm[k] = T(0) + t[k];
+    matmul3_tn(m, gz, gr);
+    rodrigues_bwd(a, gr, gv);
+  } else {
+    rodrigues_bwd(a, gz, gv);
+  }
+}
+
 // ------------------------------------------------------------- s2s1rodrigues
 // lie_tools.py:67-78: R = I + sin K + (1 - cos) K@K, K = hat(axis), (cos, sin) given.
 template <typename T>

@@ -47,6 +47,7 @@ _SIGS = {
     "lv_group_action_fwd": [_P, _P, _I64, _P, _I, _I64, _I, _I, _I, _P],
     "lv_group_action_bwd": [_P, _P, _I64, _P, _P, _P, _I64, _I, _I, _I, _P, _SZ, _P],
     "lv_exp_eazyz_vjp": [_P, _P, _P, _P, _P, _I64, _P],
+    "lv_fused_exp_action_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _I, _P, _SZ, _P],
     "lv_fused_exp_action_fwd": [_P, _P, _P, _I64, _P, _I, _P, _I64, _I, _I, _I, _P],
     "lv_fused_exp_action_fwd_repeat": [_P, _P, _P, _I64, _P, _I, _P, _I64, _I, _I, _I, _I, _P],
     "lv_softplus_fwd": [_P, _P, _I64, _P],

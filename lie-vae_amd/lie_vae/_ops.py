@@ -265,8 +265,8 @@ def _contig(t):
 
 
 class _FusedExpAction(torch.autograd.Function):
-    """mu@exp(v) -> ZYZ -> block D·F in one launch; backward = the group-action backward
-    (angle and spectrum gradients) + one fused exp -> ZYZ VJP kernel."""
+    """mu@exp(v) -> ZYZ -> block D·F in one launch; backward = one tile-kernel launch
+    (group-action backward with the exp -> ZYZ VJP in its tail) + the dF slab reduce."""
 
     @staticmethod
     def forward(ctx, mu, v, spec, L, transpose, out_dtype):
@@ -290,16 +290,14 @@ class _FusedExpAction(torch.autograd.Function):
         mu, v, spec, ang = ctx.saved_tensors
         n, L, C = v.shape[0], ctx.L, spec.shape[-1]
         gout = _prep(gout)
-        gang = torch.empty_like(ang)
         gspec = torch.empty_like(spec)
-        ws_bytes = _lib.load().lv_group_action_bwd_workspace(n, L, C, int(ctx.stride == 0))
+        ws_bytes = _lib.load().lv_group_action_bwd_workspace(n, L, C, 1)
         ws = torch.empty(max(ws_bytes, 1), device=v.device, dtype=torch.uint8)
-        call("lv_group_action_bwd", ptr(ang), ptr(spec), ctx.stride, ptr(gout), ptr(gang),
-             ptr(gspec), n, L, C, int(ctx.transpose), ptr(ws), ws_bytes, stream())
         gv = torch.empty_like(v)
         gmu = torch.empty_like(mu) if ctx.has_mu else None
-        call("lv_exp_eazyz_vjp", ptr(mu) if ctx.has_mu else None, ptr(v), ptr(gang), ptr(gmu),
-             ptr(gv), n, stream())
+        call("lv_fused_exp_action_bwd", ptr(mu) if ctx.has_mu else None, ptr(v), ptr(ang),
+             ptr(spec), ptr(gout), ptr(gmu), ptr(gv), ptr(gspec), n, L, C, int(ctx.transpose),
+             ptr(ws), ws_bytes, stream())
         return gmu, gv, gspec, None, None, None
 
 

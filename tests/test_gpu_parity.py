@@ -436,6 +436,48 @@ def test_exp_eazyz_vjp_matches_modular_bitwise(gpu_device):
         assert torch.equal(gv1, gv2), "mu" if m is not None else "exp"
 
 
+def test_fused_exp_action_bwd_matches_modular_bitwise(gpu_device):
+    """lv_fused_exp_action_bwd (group-action backward with the exp -> ZYZ VJP in the tile
+    kernel's tail, the angle gradient never leaving the chip) against lv_group_action_bwd
+    + lv_exp_eazyz_vjp, bit for bit: with and without a mean, transposed, ragged batches
+    and the grid-capped looped path (more groups than blocks), in the LDS and the large-tile
+    spectrum modes."""
+    import lie_vae._lib as lib
+    from lie_vae._lib import call, ptr, stream
+    import lie_vae.lie_tools as lt
+    torch.manual_seed(6)
+    for L, C, n, transpose in [(10, 10, 4099, False), (10, 10, 777, True), (6, 3, 50000, False),
+                               (20, 16, 301, False)]:
+        M = (L + 1) ** 2
+        v = torch.randn(n, 3, device=gpu_device)
+        mu = lt.random_group_matrices(n, device=gpu_device).contiguous()
+        F = torch.randn(M, C, device=gpu_device)
+        gout = torch.randn(n, M, C, device=gpu_device)
+        ws_bytes = lib.load().lv_group_action_bwd_workspace(n, L, C, 1)
+        ws = torch.empty(max(ws_bytes, 1), device=gpu_device, dtype=torch.uint8)
+        for m in (None, mu):
+            out = torch.empty(n, M, C, device=gpu_device)
+            ang = torch.empty(n, 3, device=gpu_device)
+            call("lv_fused_exp_action_fwd", ptr(m), ptr(v), ptr(F), 0, ptr(out), 0, ptr(ang), n,
+                 L, C, int(transpose), stream())
+            gv1, gF1 = torch.empty_like(v), torch.empty_like(F)
+            gmu1 = torch.empty_like(mu) if m is not None else None
+            call("lv_fused_exp_action_bwd", ptr(m), ptr(v), ptr(ang), ptr(F), ptr(gout),
+                 ptr(gmu1), ptr(gv1), ptr(gF1), n, L, C, int(transpose), ptr(ws), ws_bytes,
+                 stream())
+            gang, gF2 = torch.empty_like(ang), torch.empty_like(F)
+            call("lv_group_action_bwd", ptr(ang), ptr(F), 0, ptr(gout), ptr(gang), ptr(gF2), n,
+                 L, C, int(transpose), ptr(ws), ws_bytes, stream())
+            gv2 = torch.empty_like(v)
+            gmu2 = torch.empty_like(mu) if m is not None else None
+            call("lv_exp_eazyz_vjp", ptr(m), ptr(v), ptr(gang), ptr(gmu2), ptr(gv2), n, stream())
+            what = (L, C, n, transpose, m is not None)
+            assert torch.equal(gv1, gv2), what
+            assert torch.equal(gF1, gF2), what
+            if m is not None:
+                assert torch.equal(gmu1, gmu2), what
+
+
 def test_fused_vs_oracle_config2(gpu_device):
     """Config 2 exactly: B=4096, l=10, C=10, v ~ N(0,1), shared F (no mu)."""
     import lie_vae._ops as ops
