@@ -72,6 +72,16 @@ def algorithmic_bytes(batch, L, C, out_bytes):
     return batch * (12 + M * C * out_bytes) + M * C * 4
 
 
+def workload_name(L, C, B, dtype):
+    """BASELINE.json config the run matches (2: l=10, B=4096, fp32; 5: l=20, B=8192 per
+    GPU, bf16 out), else the shape itself."""
+    if (L, C, B, dtype) == (10, 10, 4096, "f32"):
+        return "config2"
+    if (L, C, B, dtype) == (20, 10, 8192, "bf16"):
+        return "config5"
+    return f"custom l={L} C={C} B={B} {dtype}"
+
+
 def cpu_threads():
     """Cores this process may use: its affinity set, capped by the box's CPU share
     (OMP_NUM_THREADS, set to the allotted share on the GPU box)."""
@@ -327,7 +337,7 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": "SO(3) samples/sec (exp+WignerD+action, l_max=10)",
+            "metric": f"SO(3) samples/sec (exp+WignerD+action, l_max={L})",
             "value": value,
             "unit": "samples/s",
             "n_gpus": world,
@@ -339,8 +349,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if args.dtype == "f32" else "f32 compute, bf16 out",
             "data": "synthetic: v ~ N(0,1)^(Bx3) per rank (seeded), F ~ N(0,1)^((L+1)^2 x C)",
-            "config": {"workload": "config2: fused exp -> ZYZ -> block Wigner-D action "
-                                   "(lv_fused_exp_action_fwd)",
+            "config": {"workload": f"{workload_name(L, C, B, args.dtype)}: fused exp -> ZYZ -> "
+                                   "block Wigner-D action (lv_fused_exp_action_fwd)",
                        "batch_per_gpu": B, "global_batch": B * world, "l_max": L,
                        "channels": C, "parallelism": f"sample-sharded x{world}, no collective",
                        "launch": args.launch},

@@ -125,8 +125,13 @@ __device__ __forceinline__ float xm_dd(const Mult<l>& m, const float (&g)[2 * l 
 // tile_flush; the LDS tile starts `mis` bytes past a 16-B boundary.
 constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per thread
 
+// Waves per SIMD the register budget is sized for: 2 gives the compiler 256 VGPRs.
+#ifndef LV_BWD_WPE
+#define LV_BWD_WPE 2
+#endif
 template <int LT, int CT, int FM>
-__global__ __launch_bounds__(512) void action_bwd_tile_kernel(ActionBwdArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LV_BWD_WPE)))
+void action_bwd_tile_kernel(ActionBwdArgs a) {
   constexpr bool SHAREDF = FM != kBwdFSample;
   constexpr bool GSLAB = FM == kBwdFSharedGlobal;
   extern __shared__ __attribute__((aligned(16))) float lds[];
