@@ -129,7 +129,13 @@ constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per threa
 #ifndef LV_BWD_WPE
 #define LV_BWD_WPE 2
 #endif
-template <int LT, int CT, int FM>
+// LOOP: blocks loop over sample groups (grid capped, bounded workspace).  Without it each
+// block takes exactly one group (grid = groups): the group loop made the compiler hoist
+// loop-invariant addresses and hold them across the whole chain (256 VGPRs + 240 B/lane of
+// spills at l = 10 vs 220 VGPRs and none; 31.4 -> 28.0 us per call at batch 4096,
+// profiles/r02_bwd_regbudget_sweep.txt), so the launcher uses it whenever the grid covers
+// the batch.
+template <int LT, int CT, int FM, bool LOOP = true>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LV_BWD_WPE)))
 void action_bwd_tile_kernel(ActionBwdArgs a) {
   constexpr bool SHAREDF = FM != kBwdFSample;
@@ -196,7 +202,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
 
-  for (int64_t g = blockIdx.x; g < a.groups; g += gridDim.x) {
+  for (int64_t g = blockIdx.x; g < a.groups; g += LOOP ? gridDim.x : a.groups) {
     const int64_t s0 = g * Sw;
     const int Sv = (int)min((int64_t)Sw, a.n - s0);
     const bool active = j < Sv;
@@ -383,6 +389,8 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSample>), grid, block, p.lds, p.stream, p.a);
   else if (p.fmode == kBwdFSharedGlobal)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSharedGlobal>), grid, block, p.lds, p.stream, p.a);
+  else if (p.a.C == kTileFastC && p.gx >= p.a.groups)
+    hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false>), grid, block, p.lds, p.stream, p.a);
   else if (p.a.C == kTileFastC)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared>), grid, block, p.lds, p.stream, p.a);
   else
