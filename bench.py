@@ -167,7 +167,7 @@ def main():
         return dry_run(args, env)
     td = launch.init_process_group(env, "nccl")
     rank, world = env.rank, env.world
-    dev = torch.device("cuda", env.local_rank)
+    dev = torch.device("cuda", launch.device_index(env))
     torch.cuda.set_device(dev)
 
     from lie_vae import _lib

@@ -84,7 +84,7 @@ def main():
         return
     torch.backends.cudnn.benchmark = args.find
     launch.init_process_group(env, "nccl")
-    dev = torch.device("cuda", env.local_rank)
+    dev = torch.device("cuda", launch.device_index(env))
     torch.cuda.set_device(dev)
 
     from lie_vae.experiments.train_dp import DPTrainer, param_count
@@ -125,10 +125,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    el = float(el.item())
+    el = launch.max_over_ranks(time.perf_counter() - t0, dev)
     peak = F32_PEAK_TFLOPS if args.amp == "off" else BF16_PEAK_TFLOPS
     if rank == 0:
         print(json.dumps({

@@ -69,10 +69,25 @@ def ensure_ranks(gpus, script, argv=None):
     raise SystemExit(rc)
 
 
+def share_gpu0():
+    """LV_SHARE_GPU0=1: rehearsal of the N-rank path on a one-GPU box -- every rank binds
+    cuda:0 and the group runs over gloo (RCCL refuses two ranks on one device).  Off by
+    default; never used for reported numbers."""
+    return os.environ.get("LV_SHARE_GPU0", "0") == "1"
+
+
+def device_index(env):
+    """The GPU this rank drives: LOCAL_RANK (one process per GPU)."""
+    return 0 if share_gpu0() else env.local_rank
+
+
 def init_process_group(env, backend):
     """Bind cuda:LOCAL_RANK (nccl = RCCL on ROCm) and join the group; no-op at world 1."""
     import torch
     import torch.distributed as dist
+    if backend == "nccl" and share_gpu0():
+        torch.cuda.set_device(0)
+        backend = "gloo"
     if backend == "nccl":
         torch.cuda.set_device(env.local_rank)
     if not env.distributed:
@@ -90,6 +105,8 @@ def max_over_ranks(value, device=None):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return float(value)
+    if dist.get_backend() == "gloo":
+        device = None
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -58,3 +58,15 @@ def test_world_size_mismatch_fails():
              {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE" in (p.stderr + p.stdout)
+
+
+def test_share_gpu0_rehearsal_mode(monkeypatch):
+    """LV_SHARE_GPU0=1 (one-GPU rehearsal) binds every rank to cuda:0; by default each
+    rank drives cuda:LOCAL_RANK."""
+    sys.path.insert(0, os.path.join(REPO, "lie-vae_amd"))
+    from lie_vae.experiments import launch
+    env = launch.RankEnv(rank=3, local_rank=3, world=4)
+    monkeypatch.delenv("LV_SHARE_GPU0", raising=False)
+    assert launch.device_index(env) == 3 and not launch.share_gpu0()
+    monkeypatch.setenv("LV_SHARE_GPU0", "1")
+    assert launch.device_index(env) == 0 and launch.share_gpu0()
