@@ -16,7 +16,7 @@ namespace lv {
 // G = gout block column:
 //   P1 = Xc F, P2 = J P1, P3 = Xb P2, P4 = J P3           (forward recompute)
 //   Q4 = Xa^T G, Q3 = J Q4, Q2 = Xb^T Q3, Q1 = J Q2, dF = Xc^T Q1
-//   d/da = <G, Xa' P4>, d/db = <Q3, Xb' P2>, d/dc = <Q1, Xc' F>
+//   d/da = <G, Xa' P4> = <Q4, K P4>, d/db = <Q2, K P2>, d/dc = <dF, K F> (kdot)
 // The dF column overwrites the lane's own G values in the tile (each degree's rows
 // belong to one wave).  Angle gradients: the C lanes of a sample and the segment waves
 // are summed in a fixed order in LDS and written straight to gang.  dF: per-sample
@@ -103,19 +103,19 @@ __device__ __forceinline__ void xm_t(const Mult<l>& m, const float (&x)[2 * l + 
     else y[i] = fmaf(m.c[-f], x[i], m.s[-f] * x[2 * l - i]);
   });
 }
+// <a, K b> with K = X(θ)^{-1} dX/dθ, the so(2) generator of the degree-l block: row i
+// of K has f_i = l - i at column 2l-i (X = C + S P with P the row reversal, so
+// dX/dθ = diag(f cos) P - diag(f sin) = X diag(f) P).  Hence <g, X' x> = <X^T g, K x>:
+// each angle gradient is a dot product of two vectors the chain computes anyway, paired
+// as f_i (a_i b_{2l-i} - a_{2l-i} b_i), with no multiples.
 template <int l>
-__device__ __forceinline__ float xm_dd(const Mult<l>& m, const float (&g)[2 * l + 1], const float (&x)[2 * l + 1]) {
+__device__ __forceinline__ float kdot(const float (&av)[2 * l + 1], const float (&bv)[2 * l + 1]) {
   float acc = 0.f;
-  sfor<2 * l + 1>([&](auto I) {
+  sfor<l>([&](auto I) {
     constexpr int i = LV_CV(I);
     constexpr int f = l - i;
-    if constexpr (f > 0) {
-      const float d = fmaf(-m.s[f], x[i], m.c[f] * x[2 * l - i]);
-      acc = fmaf(g[i], (float)f * d, acc);
-    } else if constexpr (f < 0) {
-      const float d = fmaf(m.s[-f], x[i], m.c[-f] * x[2 * l - i]);
-      acc = fmaf(g[i], (float)f * d, acc);
-    }
+    const float t = fmaf(av[i], bv[2 * l - i], -(av[2 * l - i] * bv[i]));
+    acc = fmaf((float)f, t, acc);
   });
   return acc;
 }
@@ -282,27 +282,20 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         xm<l>(mult_lds<l, 1, LT>(tj), p2, u);     // P3
         jmul<l>(u, p4);                           // P4
         sfor<nn>([&](auto K) { gq[LV_CV(K)] = active ? tile_lane[(r0 + LV_CV(K)) * C] : 0.f; });
-        {
-          const Mult<l> ma = mult_lds<l, 0, LT>(tj);
-          ga += xm_dd<l>(ma, gq, p4);
-          xm_t<l>(ma, gq, u);                     // Q4
-        }
+        xm_t<l>(mult_lds<l, 0, LT>(tj), gq, u);  // Q4
+        ga += kdot<l>(u, p4);                     // <G, Xa' P4> = <Q4, K P4>
         jmul<l>(u, p4);                           // Q3 (reuse p4)
-        {
-          const Mult<l> mb = mult_lds<l, 1, LT>(tj);
-          gb += xm_dd<l>(mb, p4, p2);
-          xm_t<l>(mb, p4, u);                     // Q2
-        }
+        xm_t<l>(mult_lds<l, 1, LT>(tj), p4, u);  // Q2
+        gb += kdot<l>(u, p2);                     // <Q3, Xb' P2> = <Q2, K P2>
         jmul<l>(u, p2);                           // Q1 (reuse p2)
+        xm_t<l>(mult_lds<l, 2, LT>(tj), p2, u);  // dF column
         {
-          const Mult<l> mc = mult_lds<l, 2, LT>(tj);
           float f0[nn];
           sfor<nn>([&](auto K) {
             constexpr int k = LV_CV(K);
             f0[k] = SHAREDF ? Fl[(r0 + k) * fstep] : Fs[(r0 + k) * C];
           });
-          gc += xm_dd<l>(mc, p2, f0);
-          xm_t<l>(mc, p2, u);                     // dF column
+          gc += kdot<l>(u, f0);                   // <Q1, Xc' F> = <dF, K F>
         }
         if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
         if constexpr (SHAREDF) {
