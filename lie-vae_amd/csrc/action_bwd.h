@@ -125,9 +125,17 @@ __device__ __forceinline__ float kdot(const float (&av)[2 * l + 1], const float 
 // tile_flush; the LDS tile starts `mis` bytes past a 16-B boundary.
 constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per thread
 
-// Waves per SIMD the register budget is sized for: 2 gives the compiler 256 VGPRs.
+// Waves per SIMD the register budget is sized for.  Up to l_max = 10 the kernel fits 168
+// VGPRs without spilling (156 at l = 10), so it is compiled for 3 waves per SIMD and the
+// plan uses twice the segments (kBwdWideMaxL in action.hip): 26.9 -> 19.5 us per call at
+// batch 4096 (profiles/r02_bwd_regbudget_sweep.txt).  Higher degrees spill at 168 and
+// keep 256 (2 waves per SIMD).  Set per instantiation unit (-DLV_INST_L).
 #ifndef LV_BWD_WPE
+#if defined(LV_INST_L) && LV_INST_L <= 10
+#define LV_BWD_WPE 3
+#else
 #define LV_BWD_WPE 2
+#endif
 #endif
 // LOOP: blocks loop over sample groups (grid capped, bounded workspace).  Without it each
 // block takes exactly one group (grid = groups): the group loop made the compiler hoist

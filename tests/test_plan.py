@@ -77,9 +77,11 @@ def test_pinned_plans_of_the_benchmark_configs():
     # config 5: bf16 tile (6*4410*2 + 16, rounded to 16 B) + separate fp32 spectrum copy + trig
     p = _lib.plan("fwd", 1, 0, BF16, 8192, 20, 10)
     assert (p["tile"], p["blocks"], p["lds_bytes"]) == (1, 1366, 52944 + 17640 + 3552)
-    # backward at the config-2 size: 2 segments (profiles/r02_bwd_nseg_sweep.txt)
+    # backward at the config-2 size: 4 segments of a 3-waves-per-SIMD build, LDS small
+    # enough for 3 blocks per CU (profiles/r02_bwd_regbudget_sweep.txt)
     b = _lib.plan("bwd", 4096, 10, 10, 1)
-    assert (b["tile"], b["segments"], b["blocks"], b["samples_per_group"]) == (1, 2, 683, 6)
+    assert (b["tile"], b["segments"], b["blocks"], b["samples_per_group"]) == (1, 4, 683, 6)
+    assert 3 * b["lds_bytes"] <= 160 * 1024
     # every (l, C) has a backward plan; large tiles take the global-spectrum fallback
     assert _lib.plan("bwd", 4096, 20, 64, 1)["tile"] == 2
     assert _lib.plan("bwd", 4096, 20, 13, 1)["tile"] == 1
