@@ -21,33 +21,45 @@ LV_EXTERN_BWD(10) LV_EXTERN_BWD(11) LV_EXTERN_BWD(12) LV_EXTERN_BWD(13) LV_EXTER
 LV_EXTERN_BWD(15) LV_EXTERN_BWD(16) LV_EXTERN_BWD(17) LV_EXTERN_BWD(18) LV_EXTERN_BWD(19)
 LV_EXTERN_BWD(20)
 
-// Shared-spectrum gradient: gF[e] = sum over the blocks' slabs in block order.  One block
-// per 64 consecutive elements; its 16 waves each sum a contiguous run of slabs (loads
-// unrolled for memory parallelism), then the 16 partials are added in wave order.
+// Shared-spectrum gradient: gF[e] = sum over the tile kernel's slabs.  One block per
+// kBwdReduceCols consecutive elements, lane = (slab stream k, column); the block's 16
+// waves split the slabs into contiguous runs, and inside a run stream k takes every
+// kBwdReduceStreams-th slab (64-byte loads, unrolled).  Against one element per lane this
+// is 4x fewer serial loads per lane and 4x the blocks (76 at l = 10, C = 10): 5.1 -> 4.4 us
+// at batch 4096.  Partials are added in a fixed order (run, then stream): deterministic.
+constexpr int kBwdReduceCols = 16;
+constexpr int kBwdReduceStreams = 64 / kBwdReduceCols;
 __global__ __launch_bounds__(64 * kBwdReduceWaves) void action_bwd_reduce_kernel(
     const float* ws_F, float* gF, int64_t MC, int nslab) {
   __shared__ float part[kBwdReduceWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int k = lane / kBwdReduceCols, col = lane - k * kBwdReduceCols;
+  const int64_t e = (int64_t)blockIdx.x * kBwdReduceCols + col;
   const int per = (nslab + kBwdReduceWaves - 1) / kBwdReduceWaves;
   const int b0 = min(nslab, w * per), b1 = min(nslab, b0 + per);
   float sum = 0.f;
   if (e < MC) {
-    int b = b0;
-    for (; b + 8 <= b1; b += 8) {
+    int b = b0 + k;
+    constexpr int S = kBwdReduceStreams;
+    for (; b + 7 * S < b1; b += 8 * S) {
       float v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = ws_F[(int64_t)(b + k) * MC + e];
+      for (int u = 0; u < 8; ++u) v[u] = ws_F[(int64_t)(b + u * S) * MC + e];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sum += v[k];
+      for (int u = 0; u < 8; ++u) sum += v[u];
     }
-    for (; b < b1; ++b) sum += ws_F[(int64_t)b * MC + e];
+    for (; b < b1; b += S) sum += ws_F[(int64_t)b * MC + e];
   }
   part[w][lane] = sum;
   __syncthreads();
-  if (w == 0 && e < MC) {
-    float r = part[0][lane];
-    for (int k = 1; k < kBwdReduceWaves; ++k) r += part[k][lane];
+  if (threadIdx.x < kBwdReduceCols && e < MC) {
+    float r = 0.f;
+    for (int ww = 0; ww < kBwdReduceWaves; ++ww) {
+      float rw = part[ww][col];
+#pragma unroll
+      for (int kk = 1; kk < kBwdReduceStreams; ++kk) rw += part[ww][kk * kBwdReduceCols + col];
+      r += rw;
+    }
     gF[e] = r;
   }
 }
@@ -389,7 +401,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.stream = st;
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
-  hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, 64)), dim3(64 * kBwdReduceWaves),
+  hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, kBwdReduceCols)), dim3(64 * kBwdReduceWaves),
                      0, st, (const float*)workspace, gF, MC, b.gx);
   LV_RETURN_LAUNCH("action_bwd_reduce_kernel");
 }
