@@ -285,10 +285,9 @@ constexpr int64_t kBwdMaxBlocks = 4096;
 // l = 10 (profiles/r02_bwd_nseg_sweep.txt): 1 / 2 / 3 / 4 / 6 / 8 segments ran
 // 40.8 / 32.0 / 42.6 / 39.1 / 44.8 / 45.5 us per call.
 constexpr double kBwdSegCost = 2.2 * 1000.0;
-// Up to l_max = kBwdWideMaxL the kernel is built for 3 waves per SIMD (LV_BWD_WPE in
-// action_bwd.h): half the per-segment cost, 4 segments at l = 10 (2 / 3 / 4 / 6 / 8 ran
-// 24.2 / 22.2 / 19.5 / 27.8 / 26.9 us per call, profiles/r02_bwd_regbudget_sweep.txt).
-constexpr int kBwdWideMaxL = 10;
+// The 3-waves-per-SIMD kernel (bwd_wide in action_bwd.h): half the per-segment cost, 4
+// segments at l = 10 (2 / 3 / 4 / 6 / 8 ran 24.2 / 22.2 / 19.5 / 27.8 / 26.9 us per call,
+// profiles/r02_bwd_regbudget_sweep.txt).
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
@@ -317,7 +316,8 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
     const size_t cap = fallback ? kBwdMaxLdsFallback : kBwdMaxLds;
     for (int Sw = 64 / C; Sw >= 1; --Sw) {
       const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
-      const double seg_cost = L <= kBwdWideMaxL ? kBwdSegCostWide : kBwdSegCost;
+      const int64_t gx = std::min<int64_t>(groups, fallback ? kBwdMaxBlocksFallback : kBwdMaxBlocks);
+      const double seg_cost = bwd_wide(L, C, fmode, groups, gx) ? kBwdSegCostWide : kBwdSegCost;
       int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / seg_cost)));
       if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
       nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));

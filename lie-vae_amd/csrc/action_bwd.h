@@ -125,26 +125,25 @@ __device__ __forceinline__ float kdot(const float (&av)[2 * l + 1], const float 
 // tile_flush; the LDS tile starts `mis` bytes past a 16-B boundary.
 constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per thread
 
-// Waves per SIMD the register budget is sized for.  Up to l_max = 10 the kernel fits 168
-// VGPRs without spilling (156 at l = 10), so it is compiled for 3 waves per SIMD and the
-// plan uses twice the segments (kBwdWideMaxL in action.hip): 26.9 -> 19.5 us per call at
-// batch 4096 (profiles/r02_bwd_regbudget_sweep.txt).  Higher degrees spill at 168 and
-// keep 256 (2 waves per SIMD).  Set per instantiation unit (-DLV_INST_L).
-#ifndef LV_BWD_WPE
-#if defined(LV_INST_L) && LV_INST_L <= 10
-#define LV_BWD_WPE 3
-#else
-#define LV_BWD_WPE 2
-#endif
-#endif
+// Up to l_max = kBwdWideMaxL the C = 10, one-group-per-block kernel fits 168 VGPRs
+// without spilling (156 at l = 10), so it has a twin built for 3 waves per SIMD
+// (WPE = 3) that the plan gives twice the segments: 26.9 -> 19.5 us per
+// call at batch 4096 (profiles/r02_bwd_regbudget_sweep.txt).  Every other variant (group
+// loop, run-time C, higher degrees) spills at 168 and keeps the 256-VGPR budget.
+constexpr int kBwdWideMaxL = 10;
+__host__ __device__ constexpr bool bwd_wide(int L, int C, int fmode, int64_t groups, int64_t gx) {
+  return L <= kBwdWideMaxL && C == kTileFastC && fmode == kBwdFShared && gx >= groups;
+}
+
 // LOOP: blocks loop over sample groups (grid capped, bounded workspace).  Without it each
 // block takes exactly one group (grid = groups): the group loop made the compiler hoist
 // loop-invariant addresses and hold them across the whole chain (256 VGPRs + 240 B/lane of
 // spills at l = 10 vs 220 VGPRs and none; 31.4 -> 28.0 us per call at batch 4096,
 // profiles/r02_bwd_regbudget_sweep.txt), so the launcher uses it whenever the grid covers
 // the batch.
-template <int LT, int CT, int FM, bool LOOP = true>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LV_BWD_WPE)))
+// WPE: waves per SIMD the register budget is sized for (3 only for the bwd_wide case).
+template <int LT, int CT, int FM, bool LOOP = true, int WPE = 2>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void action_bwd_tile_kernel(ActionBwdArgs a) {
   constexpr bool SHAREDF = FM != kBwdFSample;
   constexpr bool GSLAB = FM == kBwdFSharedGlobal;
@@ -390,7 +389,10 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSample>), grid, block, p.lds, p.stream, p.a);
   else if (p.fmode == kBwdFSharedGlobal)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSharedGlobal>), grid, block, p.lds, p.stream, p.a);
-  else if (p.a.C == kTileFastC && p.gx >= p.a.groups)
+  else if (bwd_wide(LT, p.a.C, p.fmode, p.a.groups, p.gx)) {
+    if constexpr (LT <= kBwdWideMaxL)
+      hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false, 3>), grid, block, p.lds, p.stream, p.a);
+  } else if (p.a.C == kTileFastC && p.gx >= p.a.groups)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false>), grid, block, p.lds, p.stream, p.a);
   else if (p.a.C == kTileFastC)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared>), grid, block, p.lds, p.stream, p.a);

@@ -388,7 +388,8 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     """The fallback mode (spectrum from global memory, dF slab accumulated in the block's
     workspace row) keeps the LDS mode's summation order: forced on for the config-2 shape
     (LV_BWD_FGLOBAL=1, read once per process, hence a child process), the gradients are
-    bitwise those of the LDS mode."""
+    bitwise those of the LDS mode for the same segment plan (LV_BWD_NSEG=2 in both: the
+    LDS mode's default at this shape is the 4-segment 3-waves-per-SIMD plan)."""
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -396,7 +397,7 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     outs = []
     for forced in ("0", "1"):
         path = str(tmp_path / f"g{forced}.npz")
-        env = dict(os.environ, LV_BWD_FGLOBAL=forced)
+        env = dict(os.environ, LV_BWD_FGLOBAL=forced, LV_BWD_NSEG="2")
         subprocess.run([sys.executable, "-c", _FGLOBAL_SCRIPT, pkg, path], env=env, check=True,
                        timeout=180)
         outs.append(np.load(path))
