@@ -374,3 +374,71 @@ def test_dp_trainer_graph_replay_matches_eager(gpu_device):
         torch.testing.assert_close(bg, be, rtol=1e-4, atol=1e-6)
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+
+
+_DP2_WORKER = r'''
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path[:0] = [sys.argv[1]]
+from lie_vae.experiments.train_dp import DPTrainer
+from lie_vae.experiments.vae import VAE
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+torch.backends.cudnn.benchmark = False
+torch.manual_seed(0)
+m = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10, rgb=True,
+        batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(dev)
+g = torch.Generator().manual_seed(100 + rank)          # each rank its own shard
+x = torch.rand(64, 3, 64, 64, generator=g).to(dev)
+eps = torch.randn(1, 64, 3, generator=g).to(dev)
+tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5)
+l1, _, _ = tr.step(x, eps)
+l2, _, _ = tr.step(x, eps)
+torch.cuda.synchronize()
+p = torch.cat([q.detach().flatten() for q in m.parameters()]).cpu()
+ps = [torch.empty_like(p) for _ in range(world)]
+dist.all_gather(ps, p)
+ls = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+dist.all_gather(ls, torch.tensor([float(l1), float(l2)], dtype=torch.float64))
+if rank == 0:
+    np.savez(sys.argv[2], p=torch.stack(ps).numpy(), l=torch.stack(ls).numpy())
+dist.destroy_process_group()
+'''
+
+
+def test_config4_dp_two_ranks_share_one_gpu(tmp_path):
+    """Config 4's data-parallel step with two rank processes on the one GPU of the box
+    (gloo carries the bucketed gradient all-reduce; RCCL refuses two ranks per device):
+    the config-3 model, a different 64-image shard per rank, two DPTrainer steps.  The
+    replicas must stay bit-identical (every rank applies the same all-reduced, globally
+    clipped gradient -- unsupervised.py:108-117 semantics on the global batch) and finite,
+    and the ranks' losses differ (they saw different data)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "dp2_worker.py"
+    script.write_text(_DP2_WORKER)
+    out = tmp_path / "dp2.npz"
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                    "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={port}",
+                    str(script), os.path.join(repo, "lie-vae_amd"), str(out)],
+                   env=env, check=True, timeout=200)
+    r = np.load(out)
+    p, losses = r["p"], r["l"]
+    assert np.isfinite(p).all() and np.isfinite(losses).all()
+    assert np.array_equal(p[0], p[1]), "replicas diverged"
+    assert losses[0, 0] != losses[1, 0]
