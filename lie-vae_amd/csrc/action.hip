@@ -27,7 +27,10 @@ LV_EXTERN_BWD(20)
 // kBwdReduceStreams-th slab (64-byte loads, unrolled).  Against one element per lane this
 // is 4x fewer serial loads per lane and 4x the blocks (76 at l = 10, C = 10): 5.1 -> 4.4 us
 // at batch 4096.  Partials are added in a fixed order (run, then stream): deterministic.
-constexpr int kBwdReduceCols = 16;
+#ifndef LV_REDUCE_COLS
+#define LV_REDUCE_COLS 16
+#endif
+constexpr int kBwdReduceCols = LV_REDUCE_COLS;
 constexpr int kBwdReduceStreams = 64 / kBwdReduceCols;
 __global__ __launch_bounds__(64 * kBwdReduceWaves) void action_bwd_reduce_kernel(
     const float* ws_F, float* gF, int64_t MC, int nslab) {
