@@ -292,6 +292,7 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 // segments at l = 10 (2 / 3 / 4 / 6 / 8 ran 24.2 / 22.2 / 19.5 / 27.8 / 26.9 us per call,
 // profiles/r02_bwd_regbudget_sweep.txt).
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
+constexpr int64_t kBwdCUs = 256;  // MI355X compute units
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
@@ -322,6 +323,10 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       const int64_t gx = std::min<int64_t>(groups, fallback ? kBwdMaxBlocksFallback : kBwdMaxBlocks);
       const double seg_cost = bwd_wide(L, C, fmode, groups, gx) ? kBwdSegCostWide : kBwdSegCost;
       int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / seg_cost)));
+      // small batches: at most one group per CU leaves wave slots free, so the chain is
+      // split into 8 segments (l = 10: batch 512 4 / 6 / 8 segments 11.9 / 10.5 / 10.3 us;
+      // at 2,048 (342 groups) 6 and 8 segments were slower than 4: 19.3 / 18.6 vs 14.9)
+      if (bwd_wide(L, C, fmode, groups, gx) && groups <= kBwdCUs) nseg = std::max(nseg, std::min(8, L + 1));
       if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
       nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
       if (3 * Sw > 64 * nseg || nseg > 8) continue;

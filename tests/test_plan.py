@@ -82,6 +82,9 @@ def test_pinned_plans_of_the_benchmark_configs():
     b = _lib.plan("bwd", 4096, 10, 10, 1)
     assert (b["tile"], b["segments"], b["blocks"], b["samples_per_group"]) == (1, 4, 683, 6)
     assert 3 * b["lds_bytes"] <= 160 * 1024
+    # config 3's batch (512, one group per CU at most): 8 segments
+    assert _lib.plan("bwd", 512, 10, 10, 1)["segments"] == 8
+    assert _lib.plan("bwd", 2048, 10, 10, 1)["segments"] == 4
     # every (l, C) has a backward plan; large tiles take the global-spectrum fallback
     assert _lib.plan("bwd", 4096, 20, 64, 1)["tile"] == 2
     assert _lib.plan("bwd", 4096, 20, 13, 1)["tile"] == 1

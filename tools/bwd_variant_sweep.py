@@ -12,13 +12,14 @@ import subprocess
 import sys
 
 CHILD = r"""
-import sys, json, hashlib, ctypes, torch
+import os, sys, json, hashlib, ctypes, torch
 sys.path[:0] = ['lie-vae_amd', '.']
 import bench
 from lie_vae import _lib
 dev = torch.device('cuda:0')
 torch.manual_seed(0)
-L, C, B = 10, 10, 4096
+L, C = 10, 10
+B = int(os.environ.get('SWEEP_B', '4096'))
 v = torch.randn(B, 3, device=dev); F = torch.randn(121, C, device=dev)
 g = torch.randn(B, 121, C, device=dev)
 r = bench.bench_action_bwd_kernel(v, F, g, L, dev, reps=400)
@@ -42,7 +43,7 @@ print(json.dumps({"us": r["us_per_call"], "hash": h}))
 def main():
     libs = sys.argv[1:]
     for lib in libs:
-        for ns in [2, 3, 4, 6, 8]:
+        for ns in [int(x) for x in os.environ.get('SWEEP_NSEG', '2,3,4,6,8').split(',')]:
             env = dict(os.environ, LV_BWD_NSEG=str(ns), LIEVAE_HIP_LIB=os.path.abspath(lib))
             try:
                 r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True,
