@@ -150,6 +150,7 @@ int env_int(const char* name, int dflt) {
 bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvTile = env_int("LV_TILE", 1);
   static const int kEnvWT = env_int("LV_TILE_WT", -1);
+  static const int kEnvTileNseg = env_int("LV_TILE_NSEG", 0);  // A/B testing only
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
   const int Sw = 64 / a.C;
@@ -158,6 +159,7 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
   const double target = groups < kTileManyGroups ? kTileSegCostSmall : kTileSegCostLarge;
   int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
+  if (kEnvTileNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvTileNseg);
   // the prologue takes one thread per (sample, slot): 3*Sw threads of the block
   nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
   if (3 * Sw > 64 * nseg || nseg > 8) return false;
