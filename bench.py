@@ -58,9 +58,11 @@ def parse():
     ap.add_argument("--cold-only", action="store_true",
                     help="only the scrubbed launches (for rocprofv3 kernel-trace runs)")
     ap.add_argument("--no-fwd-bwd", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sweep", action="store_true", help="also report a batch sweep")
+    ap.add_argument("--sweep", default="16384,65536",
+                    help="comma-separated batches also timed (HIP events, median of 3 rounds); "
+                         "'' to skip")
     ap.add_argument("--dry-run", action="store_true",
                     help="rehearse the rank plumbing on CPU (gloo, no HIP call)")
     return ap.parse_args()
@@ -83,8 +85,10 @@ def workload_name(L, C, B, dtype):
 
 
 def cpu_threads():
-    """Cores this process may use: its affinity set, capped by the box's CPU share
-    (OMP_NUM_THREADS, set to the allotted share on the GPU box)."""
+    """Threads for the CPU baseline: this process's affinity set, capped by the box's CPU
+    share.  On the GPU box OMP_NUM_THREADS is the allotted share (16 of a 256-core host
+    shared with other jobs' boxes); more threads would time oversubscribed cores, not the
+    reference path, so the share is what "all usable cores" means there."""
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
@@ -95,8 +99,9 @@ def cpu_threads():
 
 def cpu_baseline(L, C, batch, seconds):
     """Reference op sequence on the host (oracle/lie_ref.py, a restatement of
-    lie_tools.py:56-64,112-180,211-253), timed on a bounded sample: forward at all usable
-    cores and at 1 thread, forward+backward at all usable cores."""
+    lie_tools.py:56-64,112-180,211-253), timed on a bounded sample of the benchmark's own
+    batch (same B, l, C): forward on the usable cores and on 1 thread, forward+backward on
+    the usable cores."""
     from oracle import lie_ref
     threads, usable = cpu_threads()
     g = torch.Generator().manual_seed(0)
@@ -117,28 +122,28 @@ def cpu_baseline(L, C, batch, seconds):
             if el >= budget:
                 return n * nb / el, n, el
 
-    torch.set_num_threads(threads)
-    with torch.no_grad():
-        fw, nf, ef = timed(lambda: fwd(v, F), seconds, batch)
-    vb = v[:1024]
-
     def fb():
-        vg = vb.clone().requires_grad_(True)
+        vg = v.clone().requires_grad_(True)
         Fg = F.clone().requires_grad_(True)
         fwd(vg, Fg).square().sum().backward()
 
-    fbw, nfb, efb = timed(fb, seconds, vb.shape[0])
+    torch.set_num_threads(threads)
+    with torch.no_grad():
+        fw, nf, ef = timed(lambda: fwd(v, F), seconds, batch)
+    fbw, nfb, efb = timed(fb, seconds, batch)
     torch.set_num_threads(1)
     with torch.no_grad():
-        f1, n1, e1 = timed(lambda: fwd(v[:1024], F), seconds / 2, 1024)
+        f1, n1, e1 = timed(lambda: fwd(v, F), seconds, batch)
     torch.set_num_threads(threads)
     return {"value": fw, "unit": "samples/s", "cores": threads, "kind": "port",
             "host_cores": os.cpu_count(), "usable_cores": usable,
+            "cores_note": "OMP_NUM_THREADS share of the box (the GPU box allots 16 host "
+                          "threads of a shared 256-core host); 1-thread figure alongside",
             "value_1thread": f1, "fwd_bwd_value": fbw,
-            "sample": f"forward: {nf} batches x {batch} samples (exp+eazyz+action, l={L}, "
-                      f"C={C}, fp32) in {ef:.1f}s on {threads} threads; 1 thread: {n1} x 1024 "
-                      f"in {e1:.1f}s; forward+backward: {nfb} x 1024 in {efb:.1f}s on "
-                      f"{threads} threads; torch CPU, oracle/lie_ref.py"}
+            "sample": f"batch {batch} (exp+eazyz+action, l={L}, C={C}, fp32), torch CPU, "
+                      f"oracle/lie_ref.py: forward {nf} batches in {ef:.1f}s on {threads} "
+                      f"threads; forward+backward {nfb} batches in {efb:.1f}s on {threads} "
+                      f"threads; forward {n1} batches in {e1:.1f}s on 1 thread"}
 
 
 def dry_run(args, env):
@@ -220,38 +225,80 @@ def main():
             print(json.dumps({"cache_cold": rec}), flush=True)
         return
 
-    graph = None
+    # Timed region: K launches.  With --launch graph they are replayed from hipGraphs of
+    # `chunk` launches, and the two timing events are nodes INSIDE the first and the last
+    # graph (external event records): on a short region (the driver's 20 steps) events on
+    # the stream around graph.replay() would also time the host's submission of the first
+    # graph (~10 us before its first kernel starts), which is not kernel time.
     chunk = max(1, min(args.graph_chunk, args.steps))
+    full, rem = divmod(args.steps, chunk)
+    sizes = [chunk] * full + ([rem] if rem else [])
+    events_in_graph = args.launch == "graph"
+    ev0 = torch.cuda.Event(enable_timing=True, external=events_in_graph)
+    ev1 = torch.cuda.Event(enable_timing=True, external=events_in_graph)
+    timed, warm_graph = [], None
     if args.launch == "graph":
         launch_k(1)
         torch.cuda.synchronize(dev)
         s = torch.cuda.Stream(dev)
         s.wait_stream(stream)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=s):
-            launch_k(chunk, ctypes.c_void_p(s.cuda_stream))
-        torch.cuda.synchronize(dev)
+        cache = {}
 
-    def run_steps(k):
-        if graph is None:
+        def graph_of(n, first, last):
+            key = (n, first, last)
+            if key not in cache:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    if first:
+                        ev0.record(s)
+                    launch_k(n, ctypes.c_void_p(s.cuda_stream))
+                    if last:
+                        ev1.record(s)
+                cache[key] = g
+            return cache[key]
+
+        timed = [graph_of(n, i == 0, i == len(sizes) - 1) for i, n in enumerate(sizes)]
+        warm_graph = graph_of(chunk, False, False)
+        torch.cuda.synchronize(dev)
+        # the first replay of a fresh graph pays its one-time upload; every graph is
+        # replayed once here, outside the timed region, whatever --warmup is
+        for g in [warm_graph] + list(dict.fromkeys(timed)):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        try:
+            ok = ev0.elapsed_time(ev1) > 0
+        except RuntimeError:
+            ok = False
+        if not ok:  # no timed event nodes in graphs on this runtime: events on the stream
+            events_in_graph = False
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            timed = [graph_of(n, False, False) for n in sizes]
+
+    def warmup_steps(k):
+        if warm_graph is None:
             launch_k(k)
             return
-        full, rem = divmod(k, chunk)
-        for _ in range(full):
-            graph.replay()
-        if rem:
-            launch_k(rem)
+        f, r = divmod(k, chunk)
+        for _ in range(f):
+            warm_graph.replay()
+        if r:
+            launch_k(r)
 
-    run_steps(args.warmup)
+    warmup_steps(args.warmup)
     torch.cuda.synchronize(dev)
     if td:
         td.barrier()
     torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    run_steps(args.steps)
-    ev1.record(stream)
+    if not events_in_graph:
+        ev0.record(stream)
+    if timed:
+        for g in timed:
+            g.replay()
+    else:
+        launch_k(args.steps)
+    if not events_in_graph:
+        ev1.record(stream)
     torch.cuda.synchronize(dev)
     if td:
         td.barrier()
@@ -259,15 +306,17 @@ def main():
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
     wall_max = launch.max_over_ranks(wall, dev)
+    nranks = launch.ranks_seen(dev)  # after the timed region: ranks the collective reached
 
     value = B * args.steps * world / wall_max
     per_launch_s = gpu_ms / 1e3 / args.steps
     achieved = abytes / per_launch_s / 1e9
 
     sweep = None
-    if args.sweep and rank == 0:
+    sweep_batches = [int(b) for b in args.sweep.split(",") if b.strip()]
+    if sweep_batches and rank == 0:
         sweep = []
-        for nb in (4096, 16384, 65536, 262144):
+        for nb in sweep_batches:
             vv = torch.randn(nb, 3, device=dev)
             oo = torch.empty(nb, M, C, device=dev, dtype=out_dtype)
             # >= ~10 ms of launches per round: the first rounds after a fresh output
@@ -341,6 +390,8 @@ def main():
             "value": value,
             "unit": "samples/s",
             "n_gpus": world,
+            "ranks_seen": nranks,
+            "max_over_ranks": world > 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": wall_max * 1e3 / args.steps,
@@ -358,6 +409,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": abytes,
                          "us_per_launch_events": per_launch_s * 1e6,
+                         "events": "graph nodes" if events_in_graph else "stream",
                          "cache": "hot (back-to-back launches)"},
             "cache_cold": cache_cold,
             "cpu_baseline": cpu,

@@ -56,6 +56,10 @@ def main():
     ap.add_argument("--no-find", dest="find", action="store_false",
                     help="keep MIOpen's heuristic conv solutions (default: torch.backends."
                          "cudnn.benchmark, MIOpen times the candidates once per shape)")
+    ap.add_argument("--conv-gemm", choices=["on", "off"], default="on",
+                    help="run the two GEMM-shaped layers (decoder 1x1->4x4 ConvTranspose2d, "
+                         "encoder 4x4->1x1 head) as addmm on hipBLASLt (on) or through MIOpen "
+                         "(off); nets.GEMM_LAYERS")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd, bwd, all-reduce, clip, Adam) in a "
                          "hipGraph and time its replays")
@@ -87,8 +91,10 @@ def main():
     dev = torch.device("cuda", launch.device_index(env))
     torch.cuda.set_device(dev)
 
+    from lie_vae.experiments import nets
     from lie_vae.experiments.train_dp import DPTrainer, param_count
     from lie_vae.experiments.vae import VAE
+    nets.GEMM_LAYERS = args.conv_gemm == "on"
 
     torch.manual_seed(0)
     model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,
@@ -137,6 +143,7 @@ def main():
                        "params": param_count(model),
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
+                       "conv_gemm": args.conv_gemm,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,

@@ -83,16 +83,21 @@ inline double degree_cost(int l, bool bwd) {
 }
 
 // Split degrees 0..L into nseg contiguous ranges minimising the max range cost
-// (prologue cost P charged per range).  Returns seg_lo[0..nseg].
+// (prologue cost P charged per range).  Returns seg_lo[0..nseg].  Fixed-size tables: no
+// allocation on the launch path.
 inline int plan_segments(int L, int nseg, double P, bool bwd, int* seg_lo) {
+  constexpr int kD = LV_MAX_DEGREE + 1;
   const int D = L + 1;
   nseg = std::max(1, std::min(nseg, std::min(D, kMaxSeg)));
-  std::vector<double> pre(D + 1, 0.0);
+  double pre[kD + 1];
+  pre[0] = 0.0;
   for (int l = 0; l < D; ++l) pre[l + 1] = pre[l] + degree_cost(l, bwd);
   // dp[k][i]: best max cost splitting first i degrees into k ranges
   const double INF = 1e30;
-  std::vector<std::vector<double>> dp(nseg + 1, std::vector<double>(D + 1, INF));
-  std::vector<std::vector<int>> arg(nseg + 1, std::vector<int>(D + 1, 0));
+  double dp[kMaxSeg + 1][kD + 1];
+  int arg[kMaxSeg + 1][kD + 1];
+  for (int k = 0; k <= nseg; ++k)
+    for (int i = 0; i <= D; ++i) { dp[k][i] = INF; arg[k][i] = 0; }
   dp[0][0] = 0.0;
   for (int k = 1; k <= nseg; ++k)
     for (int i = 1; i <= D; ++i)
@@ -140,17 +145,25 @@ constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum sl
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
 
-// LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy (A/B
-// testing and diagnosis only; read once per process).
+// A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
+// LV_*_NSEG force segment counts, LV_BWD_FGLOBAL forces the backward's global-spectrum
+// mode) exist only in the A/B build (-DLV_AB_KNOBS -> liblievae_hip_ab.so, used by
+// tools/ and one bitwise test): the product library never reads the environment, so a
+// stray variable cannot change its kernels or its summation order.
+#ifdef LV_AB_KNOBS
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
+#define LV_KNOB(name, dflt) env_int(name, dflt)
+#else
+#define LV_KNOB(name, dflt) (dflt)
+#endif
 
 bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
-  static const int kEnvTile = env_int("LV_TILE", 1);
-  static const int kEnvWT = env_int("LV_TILE_WT", -1);
-  static const int kEnvTileNseg = env_int("LV_TILE_NSEG", 0);  // A/B testing only
+  static const int kEnvTile = LV_KNOB("LV_TILE", 1);
+  static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
+  static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
   const int Sw = 64 / a.C;
@@ -230,7 +243,7 @@ int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C
   const int ob = out_dtype == LV_DTYPE_BF16 ? 2 : 4;
   if (Fstride == 0 && plan_tile(p, L, ob)) return LV_OK;
   const double P = fused ? kPrologueFused : kPrologueFwd;
-  static const int kEnvFwdNseg = env_int("LV_FWD_NSEG", 0);  // A/B testing only
+  static const int kEnvFwdNseg = LV_KNOB("LV_FWD_NSEG", 0);  // A/B testing only
   const int nseg = kEnvFwdNseg > 0 ? std::min(kEnvFwdNseg, std::min(L + 1, kMaxSeg))
                                    : choose_nseg(n, p.a.Sw, L, P, false);
   plan_segments(L, nseg, P, false, p.a.seg_lo);
@@ -250,6 +263,40 @@ int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C
   return LV_OK;
 }
 
+// Per-thread caches of launch plans, keyed by everything the planners read: the segment
+// DP and the LDS sizing run once per shape instead of on every call (the eager training
+// path calls the same shapes every step).
+template <class K, class V, int N = 8>
+struct PlanCache {
+  K key[N];
+  V val[N];
+  int used = 0, next = 0;
+  const V* find(const K& k) const {
+    for (int i = 0; i < used; ++i)
+      if (key[i] == k) return &val[i];
+    return nullptr;
+  }
+  void put(const K& k, const V& v) {
+    key[next] = k;
+    val[next] = v;
+    next = (next + 1) % N;
+    used = std::min(used + 1, N);
+  }
+};
+using FwdKey = std::array<int64_t, 6>;  // fused, F stride, out dtype, n, L, C
+
+int plan_fwd_cached(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C, FwdLaunch& p) {
+  thread_local PlanCache<FwdKey, FwdLaunch> cache;
+  const FwdKey k{fused ? 1 : 0, Fstride, out_dtype, n, L, C};
+  if (const FwdLaunch* hit = cache.find(k)) {
+    p = *hit;
+    return LV_OK;
+  }
+  if (int e = plan_fwd(fused, Fstride, out_dtype, n, L, C, p)) return e;
+  cache.put(k, p);
+  return LV_OK;
+}
+
 int action_fwd_common(bool fused, const float* ang, const float* mu, const float* v, const float* F,
                       int64_t Fstride, void* out, int out_dtype, float* ang_out, int64_t n, int L,
                       int C, int transpose, hipStream_t stream) {
@@ -259,7 +306,7 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   LV_CHECK_ARG(F && out, "null F/out");
   LV_CHECK_ARG(fused ? (v != nullptr) : (ang != nullptr), "null input");
   FwdLaunch p;
-  if (int e = plan_fwd(fused, Fstride, out_dtype, n, L, C, p)) return e;
+  if (int e = plan_fwd_cached(fused, Fstride, out_dtype, n, L, C, p)) return e;
   p.a.ang = ang;
   p.a.mu = mu;
   p.a.v = v;
@@ -311,8 +358,8 @@ struct BwdPlan {
 };
 
 bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
-  static const int kEnvNseg = env_int("LV_BWD_NSEG", 0);      // A/B testing only
-  static const int kEnvGlobal = env_int("LV_BWD_FGLOBAL", 0);  // force the fallback (tests)
+  static const int kEnvNseg = LV_KNOB("LV_BWD_NSEG", 0);      // A/B testing only
+  static const int kEnvGlobal = LV_KNOB("LV_BWD_FGLOBAL", 0);  // force the fallback (tests)
   b = BwdPlan{};
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
   double total = 0.0;
@@ -356,6 +403,20 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   return false;
 }
 
+using BwdKey = std::array<int64_t, 4>;  // n, L, C, shared spectrum
+
+bool plan_bwd_cached(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
+  thread_local PlanCache<BwdKey, BwdPlan> cache;
+  const BwdKey k{n, L, C, sharedF ? 1 : 0};
+  if (const BwdPlan* hit = cache.find(k)) {
+    b = *hit;
+    return true;
+  }
+  if (!plan_bwd(n, L, C, sharedF, b)) return false;
+  cache.put(k, b);
+  return true;
+}
+
 }  // namespace
 }  // namespace lv
 
@@ -379,7 +440,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   LV_CHECK_ARG(ang && F && gout && gF && (gang || v), "null pointer argument");
   LV_CHECK_ARG(!v || (gv && (!mu || gmu)), "null VJP output");
   BwdPlan b;
-  LV_CHECK_ARG(plan_bwd(n, L, C, sharedF, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
+  LV_CHECK_ARG(plan_bwd_cached(n, L, C, sharedF, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
   if (sharedF && (ws_bytes < b.ws || !workspace)) {
     set_error("workspace too small: need %zu bytes", b.ws);
     return LV_ERR_WORKSPACE;
@@ -447,7 +508,7 @@ int lv_fused_exp_action_fwd_repeat(const float* mu, const float* v, const float*
 size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F) {
   if (n <= 0 || L < 0 || L > LV_MAX_DEGREE || C < 1 || C > LV_MAX_CHANNELS) return 0;
   BwdPlan b;
-  if (!plan_bwd(n, L, C, shared_F != 0, b)) return 0;
+  if (!plan_bwd_cached(n, L, C, shared_F != 0, b)) return 0;
   return b.ws;
 }
 

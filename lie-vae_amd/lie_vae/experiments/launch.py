@@ -110,3 +110,17 @@ def max_over_ranks(value, device=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def ranks_seen(device=None):
+    """SUM all-reduce of a one from every rank over the live process group (RCCL under
+    ``nccl``): the number of ranks the collective actually reached (1 without a group)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    if dist.get_backend() == "gloo":
+        device = None
+    t = torch.ones(1, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(round(float(t.item())))

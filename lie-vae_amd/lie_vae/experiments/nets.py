@@ -3,8 +3,84 @@
 
 These dense convolutions are MFMA work and run through PyTorch-ROCm (MIOpen /
 hipBLASLt); they are callers of the hot path, not part of it.
+
+Two layers of the stacks are plain GEMMs in disguise and run as one:
+  * the decoder's first ConvTranspose2d(M·C, h, 4, 1, 0) sees a 1x1 input (nets.py:66):
+    out[b, (o, i, j)] = x[b, :] · W[:, o, i, j] + bias[o], a [B x M·C]·[M·C x 16h] GEMM;
+  * the encoder's head Conv2d(8h, out, 4, 1, 0) sees a 4x4 input (nets.py:54):
+    out[b, o] = <x[b], W[o]> + bias[o], a [B x 128h]·[128h x out] GEMM.
+``GemmConvTranspose2d`` / ``GemmConv2d`` keep the nn.ConvTranspose2d / nn.Conv2d
+parameters (same state_dict) and compute those shapes with one addmm (hipBLASLt, on
+MFMA; bf16 under autocast) instead of MIOpen's convolution solvers; any other input
+shape takes the convolution.  ``GEMM_LAYERS = False`` before building a model restores
+plain convolutions (A/B).
 """
+import torch
 from torch import nn
+
+GEMM_LAYERS = True
+
+
+def _cl(t):
+    return t.dim() == 4 and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
+
+
+class GemmConvTranspose2d(nn.ConvTranspose2d):
+    """ConvTranspose2d that runs a stride-1, unpadded layer on a 1x1 input as one GEMM."""
+
+    def _gemm_shape(self, x):
+        return (x.dim() == 4 and x.shape[-2:] == (1, 1) and self.stride == (1, 1)
+                and self.padding == (0, 0) and self.output_padding == (0, 0)
+                and self.dilation == (1, 1) and self.groups == 1)
+
+    def forward(self, x, output_size=None):
+        if output_size is not None or not self._gemm_shape(x):
+            return super().forward(x, output_size)
+        B, (k0, k1) = x.shape[0], self.kernel_size
+        cl = _cl(self.weight)
+        # W (c_in, c_out, k0, k1) -> columns (o, i, j) [NCHW out] or (i, j, o) [NHWC out]
+        w = (self.weight.permute(0, 2, 3, 1) if cl else self.weight).reshape(self.in_channels, -1)
+        xm = x.reshape(B, self.in_channels)
+        if self.bias is None:
+            y = xm @ w
+        else:
+            b = self.bias.repeat(k0 * k1) if cl else self.bias.repeat_interleave(k0 * k1)
+            y = torch.addmm(b, xm, w)
+        if cl:
+            return y.view(B, k0, k1, self.out_channels).permute(0, 3, 1, 2)
+        return y.view(B, self.out_channels, k0, k1)
+
+
+class GemmConv2d(nn.Conv2d):
+    """Conv2d that runs a stride-1, unpadded layer whose input is exactly one kernel
+    window (k x k -> 1x1) as one GEMM."""
+
+    def _gemm_shape(self, x):
+        return (x.dim() == 4 and tuple(x.shape[-2:]) == tuple(self.kernel_size)
+                and self.stride == (1, 1) and self.padding == (0, 0)
+                and self.dilation == (1, 1) and self.groups == 1
+                and self.padding_mode == "zeros")
+
+    def forward(self, x):
+        if not self._gemm_shape(x):
+            return super().forward(x)
+        B = x.shape[0]
+        if _cl(x):  # NHWC memory: flatten (i, j, c) without a copy, reorder the weight
+            xm = x.permute(0, 2, 3, 1).reshape(B, -1)
+            w = self.weight.permute(0, 2, 3, 1).reshape(self.out_channels, -1)
+        else:
+            xm = x.reshape(B, -1)
+            w = self.weight.reshape(self.out_channels, -1)
+        y = torch.nn.functional.linear(xm, w, self.bias)
+        return y.view(B, self.out_channels, 1, 1)
+
+
+def _conv(*a):
+    return (GemmConv2d if GEMM_LAYERS else nn.Conv2d)(*a)
+
+
+def _convt(*a):
+    return (GemmConvTranspose2d if GEMM_LAYERS else nn.ConvTranspose2d)(*a)
 
 
 class View(nn.Module):
@@ -30,7 +106,7 @@ def _down_stack(in_dims, hidden, out_dims, batch_norm):
             layers.append(nn.BatchNorm2d(width))
         layers.append(nn.LeakyReLU(0.2, inplace=True))
         c = width
-    layers += [nn.Conv2d(c, out_dims, 4, 1, 0), Flatten()]
+    layers += [_conv(c, out_dims, 4, 1, 0), Flatten()]
     return layers
 
 
@@ -52,7 +128,7 @@ class DeconvNet(nn.Sequential):
     """1x1 -> 64x64 transposed-conv stack — nets.py:60-75."""
 
     def __init__(self, in_dims, hidden_dims, rgb=False):
-        layers = [View(-1, in_dims, 1, 1), nn.ConvTranspose2d(in_dims, hidden_dims, 4, 1, 0), nn.ReLU()]
+        layers = [View(-1, in_dims, 1, 1), _convt(in_dims, hidden_dims, 4, 1, 0), nn.ReLU()]
         for _ in range(3):
             layers += [nn.ConvTranspose2d(hidden_dims, hidden_dims, 4, 2, 1), nn.ReLU()]
         layers.append(nn.ConvTranspose2d(hidden_dims, 3 if rgb else 1, 4, 2, 1))

@@ -139,12 +139,20 @@ class DPTrainer:
     ``graph=True`` builds Adam with device-side step state (``capturable``) so that
     :meth:`capture` can record the whole step -- forward, backward, the bucketed
     all-reduce, clip and Adam -- as one hipGraph and replay it without host launches.
+
+    ``sync_bn=True`` converts the encoder's BatchNorm layers to ``SyncBatchNorm``: batch
+    statistics over the global batch (one all-gather of per-rank moments per layer), so
+    the DP step equals the single-device step on the concatenated batch, as the
+    reference's one-device training computes it.  Off by default: per-rank statistics
+    need no forward collective.
     """
 
     def __init__(self, model, lr=1e-3, weight_decay=0.0, clip_grads=1e-5, beta=1.0,
                  elbo_samples=1, bucket_bytes=32 << 20, group=None, broadcast=True,
                  control=None, control_p=1, selective_clip=False, nan_check=False,
-                 amp_dtype=None, graph=False):
+                 amp_dtype=None, graph=False, sync_bn=False):
+        if sync_bn and dist.is_initialized() and dist.get_world_size(group) > 1:
+            model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model, process_group=group)
         self.model = model
         self.amp_dtype = amp_dtype
         self.clip = clip_grads
@@ -219,20 +227,28 @@ class DPTrainer:
             ts += [t for t in self.opt.state.get(p, {}).values() if torch.is_tensor(t)]
         return ts
 
+    # the per-forward samples the latent modules and the VAE keep on ``self``
+    # (reparameterize.py:41,94-95,192; vae.py:103)
+    _SAMPLE_FIELDS = ("z", "v", "mu_lie", "sigma", "mu")
+
     def _drop_autograd_refs(self):
-        """The model keeps its last sample (VAE.z, the latent modules' z / v / sigma) with
-        the autograd graph attached; that graph holds the parameters' AccumulateGrad nodes,
-        which would then keep the eager stream and break capture on the side stream."""
+        """The model keeps its last sample (VAE.z, the latent modules' z / v / mu_lie /
+        sigma) with the autograd graph attached; that graph holds the parameters'
+        AccumulateGrad nodes, which would then keep the eager stream and break capture on
+        the side stream.  Only those known sample fields are detached; nothing else on the
+        modules is touched."""
         def strip(v):
-            if torch.is_tensor(v) and v.grad_fn is not None:
-                return v.detach()
+            if torch.is_tensor(v):
+                return v.detach() if v.grad_fn is not None else v
+            if isinstance(v, tuple) and hasattr(v, "_fields"):  # namedtuple
+                return type(v)(*(strip(u) for u in v))
             if isinstance(v, (list, tuple)):
                 return type(v)(strip(u) for u in v)
             return v
         for m in self.model.modules():
-            for k, v in list(vars(m).items()):
-                if not k.startswith("_"):
-                    setattr(m, k, strip(v))
+            for k in self._SAMPLE_FIELDS:
+                if k in vars(m) and not isinstance(vars(m)[k], torch.nn.Module):
+                    setattr(m, k, strip(vars(m)[k]))
 
     def capture(self, x, eps=None, warmup=3):
         """Record one training step as a hipGraph; returns ``replay(x=None, eps=None)``
@@ -250,6 +266,10 @@ class DPTrainer:
             raise ValueError("capture() needs a constant, non-zero beta")
         if self.nan_check:
             raise ValueError("capture() cannot run the per-step NaN check")
+        if self.ar.world > 1 and dist.get_backend(self.ar.group) != "nccl":
+            raise ValueError("capture() with world > 1 needs the nccl (RCCL) backend: a "
+                             f"{dist.get_backend(self.ar.group)} all-reduce cannot be captured "
+                             "in a hipGraph")
         beta = self.beta_schedule.value
         dev = x.device
         self._drop_autograd_refs()
@@ -282,6 +302,9 @@ class DPTrainer:
             if x_new is not None:
                 gx.copy_(x_new)
             if eps_new is not None:
+                if geps is None:
+                    raise ValueError("this graph was captured without eps (the model draws "
+                                     "its own noise); capture with eps to inject it")
                 geps.copy_(eps_new)
             self.it += 1
             graph.replay()

@@ -213,9 +213,11 @@ class SO3reparameterize(nn.Module):
         return _ops.so3_log_posterior(v, sigma, self.k)
 
     def log_prior(self):
-        # = torch.tensor([-log 8pi^2], device=...) (reparameterize.py:265-267) without the
-        # host-to-device copy, so the step stays capturable in a hipGraph
-        prior = self.z.new_full((1,), - np.log(8 * (np.pi ** 2)), dtype=torch.get_default_dtype())
+        # torch.tensor([-log 8pi^2], device=...) (reparameterize.py:265-267) is float64 (torch
+        # infers it from the numpy scalar), so the KL and the IWAE weights are float64 there
+        # too; a device fill of the same value keeps the dtype and needs no host-to-device
+        # copy, so the step stays capturable in a hipGraph
+        prior = self.z.new_full((1,), - np.log(8 * (np.pi ** 2)), dtype=torch.float64)
         return prior.expand_as(self.z[..., 0, 0])
 
     def nsample(self, n=1):

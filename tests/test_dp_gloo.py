@@ -167,3 +167,28 @@ def test_linear_schedule_matches_reference_rule():
     assert s(0) == 4 and s(1) == 4 and s(2) == 6 and s(4) == 10 and s(5) == 10
     s = train_dp.LinearSchedule(10, 4, 1, 4)
     assert s(0) == 10 and s(2) == 8 and s(5) == 4
+
+
+def _capture_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = train_dp.DPTrainer(TinyVAE(), lr=1e-2, graph=True)
+    try:
+        tr.capture(torch.randn(4, 12))
+        msg = "no error"
+    except ValueError as e:
+        msg = str(e)
+    with open(os.path.join(outdir, f"cap{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.destroy_process_group()
+
+
+def test_capture_refuses_uncapturable_collective():
+    """A gloo all-reduce cannot be recorded in a hipGraph: capture() at world > 1 refuses
+    any backend but nccl (RCCL) with a ValueError before touching the device."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_capture_worker, args=(2, port, d), nprocs=2, join=True)
+        for r in range(2):
+            with open(os.path.join(d, f"cap{r}.txt")) as f:
+                assert "needs the nccl" in f.read()

@@ -376,7 +376,7 @@ def test_dp_trainer_graph_replay_matches_eager(gpu_device):
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
 
 
-_DP2_WORKER = r'''
+_DP2_WORKER = r"""
 import os, sys
 import numpy as np
 import torch
@@ -384,39 +384,86 @@ import torch.distributed as dist
 sys.path[:0] = [sys.argv[1]]
 from lie_vae.experiments.train_dp import DPTrainer
 from lie_vae.experiments.vae import VAE
+PER_RANK = int(sys.argv[3])
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 torch.backends.cudnn.benchmark = False
-torch.manual_seed(0)
-m = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10, rgb=True,
-        batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(dev)
-g = torch.Generator().manual_seed(100 + rank)          # each rank its own shard
-x = torch.rand(64, 3, 64, 64, generator=g).to(dev)
-eps = torch.randn(1, 64, 3, generator=g).to(dev)
-tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5)
-l1, _, _ = tr.step(x, eps)
-l2, _, _ = tr.step(x, eps)
-torch.cuda.synchronize()
-p = torch.cat([q.detach().flatten() for q in m.parameters()]).cpu()
-ps = [torch.empty_like(p) for _ in range(world)]
-dist.all_gather(ps, p)
-ls = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
-dist.all_gather(ls, torch.tensor([float(l1), float(l2)], dtype=torch.float64))
-if rank == 0:
-    np.savez(sys.argv[2], p=torch.stack(ps).numpy(), l=torch.stack(ls).numpy())
+torch.backends.cudnn.deterministic = True     # MIOpen: deterministic solutions
+
+
+def model():
+    torch.manual_seed(0)
+    return VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10, rgb=True,
+               batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(dev)
+
+
+def flat(ps, grad=False):
+    return torch.cat([(q.grad if grad else q.detach()).flatten() for q in ps]).cpu()
+
+
+g = torch.Generator().manual_seed(100)          # the global batch; rank r takes shard r
+xs = [torch.rand(world * PER_RANK, 3, 64, 64, generator=g) for _ in range(2)]
+es = [torch.randn(1, world * PER_RANK, 3, generator=g) for _ in range(2)]
+sh = slice(rank * PER_RANK, (rank + 1) * PER_RANK)
+m = model()
+tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5, sync_bn=True)
+names = [n for n, _ in m.named_parameters()]
+res = {"sizes": np.array([q.numel() for q in m.parameters()])}
+for it in range(2):
+    if rank == 0:
+        # the single-device step's gradient on the concatenated batch AT THE REPLICAS'
+        # CURRENT PARAMETERS (unsupervised.py:108-116: loss mean, backward, global clip),
+        # plain BatchNorm, no collective
+        ref = model()
+        ref.load_state_dict(m.state_dict())
+        recon, kl, _ = ref.elbo(xs[it].to(dev), 1, eps=es[it].to(dev))
+        lref = (recon + kl).mean()
+        lref.backward()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), 1e-5)
+        res[f"at_grad{it}"] = flat(ref.parameters(), True).numpy()
+        res[f"at_loss{it}"] = np.array([float(lref)])
+        del ref
+    l, _, _ = tr.step(xs[it][sh].to(dev), es[it][:, sh].to(dev))
+    torch.cuda.synchronize()
+    for name, t in (("grad", flat(m.parameters(), True)), ("p", flat(m.parameters())),
+                    ("loss", l.double().reshape(1).cpu())):
+        ts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(ts, t)
+        res[f"{name}{it}"] = torch.stack(ts).numpy()
 dist.destroy_process_group()
-'''
+if rank == 0:
+    # the single-device trajectory: two reference steps on the concatenated batches from
+    # the same initial state
+    m1 = model()
+    t1 = DPTrainer(m1, lr=1e-3, clip_grads=1e-5)
+    for it in range(2):
+        t1.step(xs[it].to(dev), es[it].to(dev))
+        torch.cuda.synchronize()
+        res[f"ref_p{it}"] = flat(m1.parameters()).numpy()
+    np.savez(sys.argv[2], names=np.array(names), **res)
+"""
+
+
+def _worst_tensors(err, sizes, names, k=3):
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    per = [(float(np.linalg.norm(err[offs[i]:offs[i + 1]])), str(names[i]))
+           for i in range(len(sizes))]
+    return sorted(per, reverse=True)[:k]
 
 
 def test_config4_dp_two_ranks_share_one_gpu(tmp_path):
-    """Config 4's data-parallel step with two rank processes on the one GPU of the box
-    (gloo carries the bucketed gradient all-reduce; RCCL refuses two ranks per device):
-    the config-3 model, a different 64-image shard per rank, two DPTrainer steps.  The
-    replicas must stay bit-identical (every rank applies the same all-reduced, globally
-    clipped gradient -- unsupervised.py:108-117 semantics on the global batch) and finite,
-    and the ranks' losses differ (they saw different data)."""
+    """Config 4's data-parallel step at its per-GPU shard (512 images per rank) with two
+    rank processes on the one GPU of the box (gloo carries the bucketed gradient all-reduce
+    and the SyncBatchNorm moments; RCCL refuses two ranks per device), against the
+    single-device step on the concatenated 1,024-image batch (unsupervised.py:108-117 on
+    one device, main.py:17), MIOpen pinned deterministic:
+      * the replicas stay bit-identical over two steps, and the ranks saw different data;
+      * at each step the all-reduced, globally clipped gradient equals the single-device
+        gradient at the same parameters to fp32 summation noise (normwise), and the global
+        loss is the mean of the ranks' losses;
+      * two DP steps land on the single-device trajectory from the same initial state."""
     import os
     import socket
     import subprocess
@@ -435,10 +482,23 @@ def test_config4_dp_two_ranks_share_one_gpu(tmp_path):
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                     "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={port}",
-                    str(script), os.path.join(repo, "lie-vae_amd"), str(out)],
-                   env=env, check=True, timeout=200)
+                    str(script), os.path.join(repo, "lie-vae_amd"), str(out), "512"],
+                   env=env, check=True, timeout=300)
     r = np.load(out)
-    p, losses = r["p"], r["l"]
-    assert np.isfinite(p).all() and np.isfinite(losses).all()
-    assert np.array_equal(p[0], p[1]), "replicas diverged"
-    assert losses[0, 0] != losses[1, 0]
+    sizes, names = r["sizes"], r["names"]
+    report = []
+    for it in range(2):
+        p, grad, loss = r[f"p{it}"], r[f"grad{it}"], r[f"loss{it}"]
+        assert np.isfinite(p).all() and np.isfinite(grad).all() and np.isfinite(loss).all()
+        assert np.array_equal(p[0], p[1]), f"replicas diverged at step {it + 1}"
+        assert np.array_equal(grad[0], grad[1])
+        assert loss[0, 0] != loss[1, 0]  # different shards
+        assert loss.mean() == pytest.approx(float(r[f"at_loss{it}"][0]), rel=1e-5)
+        rg = r[f"at_grad{it}"]
+        err = np.linalg.norm(grad[0] - rg) / np.linalg.norm(rg)
+        perr = np.linalg.norm(p[0] - r[f"ref_p{it}"]) / np.linalg.norm(r[f"ref_p{it}"])
+        report.append((it + 1, err, perr, _worst_tensors(grad[0] - rg, sizes, names)))
+    print(report)
+    for step, err, perr, worst in report:
+        assert err <= 1e-4, f"step {step}: gradient vs single device {err:.2e}; {worst}"
+        assert perr <= 1e-5, f"step {step}: parameters vs single-device trajectory {perr:.2e}"

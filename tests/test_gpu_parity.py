@@ -389,7 +389,9 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     workspace row) keeps the LDS mode's summation order: forced on for the config-2 shape
     (LV_BWD_FGLOBAL=1, read once per process, hence a child process), the gradients are
     bitwise those of the LDS mode for the same segment plan (LV_BWD_NSEG=2 in both: the
-    LDS mode's default at this shape is the 4-segment 3-waves-per-SIMD plan)."""
+    LDS mode's default at this shape is the 4-segment 3-waves-per-SIMD plan).  The knobs
+    exist only in the A/B build of the same kernels (liblievae_hip_ab.so, -DLV_AB_KNOBS);
+    the product library ignores the environment (test_product_library_ignores_knobs)."""
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -397,7 +399,8 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     outs = []
     for forced in ("0", "1"):
         path = str(tmp_path / f"g{forced}.npz")
-        env = dict(os.environ, LV_BWD_FGLOBAL=forced, LV_BWD_NSEG="2")
+        env = dict(os.environ, LV_BWD_FGLOBAL=forced, LV_BWD_NSEG="2",
+                   LIEVAE_HIP_LIB=os.path.join(pkg, "lie_vae", "liblievae_hip_ab.so"))
         subprocess.run([sys.executable, "-c", _FGLOBAL_SCRIPT, pkg, path], env=env, check=True,
                        timeout=180)
         outs.append(np.load(path))
@@ -516,6 +519,8 @@ def test_so3_reparam_vs_golden(gpu_device, mode):
     lp = host(rep.log_posterior())
     np.testing.assert_allclose(lp, g[f"{mode}_logpost"], rtol=1e-5, atol=1e-4)
     kl = rep.kl()
+    # the reference's prior is a float64 tensor (reparameterize.py:265-267): kl follows it
+    assert kl.dtype == torch.float64 and g[f"{mode}_kl"].dtype == np.float64, kl.dtype
     np.testing.assert_allclose(host(kl), g[f"{mode}_kl"], rtol=1e-5, atol=1e-4)
     ((z * dev(g[f"{mode}_gz"], gpu_device)).sum() +
      (kl * dev(g[f"{mode}_gk"], gpu_device)).sum()).backward()
@@ -634,12 +639,14 @@ def test_vae_toy_elbo_and_log_likelihood_vs_oracle(gpu_device):
                     what="x_recon")
     np.testing.assert_allclose(host(recon), recon_ref.numpy(), rtol=1e-4)
     np.testing.assert_allclose(host(kl_sum), kl_ref.numpy(), rtol=1e-4, atol=1e-4)
+    assert kl_sum.dtype == torch.float64  # the reference's float64 prior (reparameterize.py:265-267)
     # IWAE: log_likelihood draws eps with torch.randn on the device; replay the same draw
     torch.cuda.manual_seed(11)
     eps2 = torch.randn((n, B, 3), device=gpu_device)
     torch.cuda.manual_seed(11)
     with torch.no_grad():
         ll = vg.log_likelihood(xg, n)
+    assert ll.dtype == torch.float64
     _, recon2, lq2, _ = _vae_oracle(vae, x, eps2.cpu(), L)
     w = -recon2 - math.log(8 * math.pi ** 2) - lq2
     ll_ref = (torch.logsumexp(w, 0) - math.log(n)).mean()

@@ -105,3 +105,39 @@ def test_pinned_plans_of_the_benchmark_configs():
 def test_plan_rejects_bad_arguments(args):
     with pytest.raises(_lib.LieVaeHipError):
         _lib.plan(*args)
+
+
+_KNOB_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from lie_vae import _lib
+print(json.dumps([_lib.plan("fwd", 1, 0, _lib.LV_DTYPE_F32, 4096, 10, 10),
+                  _lib.plan("bwd", 4096, 10, 10, 1)]))
+"""
+
+
+@pytest.mark.parametrize("lib,honours", [("liblievae_hip.so", False), ("liblievae_hip_ab.so", True)])
+def test_product_library_ignores_knobs(lib, honours):
+    """The A/B knobs (LV_TILE, LV_TILE_NSEG, LV_BWD_NSEG, LV_BWD_FGLOBAL, ...) are compiled
+    into liblievae_hip_ab.so only (-DLV_AB_KNOBS): with them set in the environment the
+    product library plans exactly as without, the A/B build changes its plans."""
+    import json
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lie-vae_amd")
+    path = os.path.join(pkg, "lie_vae", lib)
+
+    def run(extra):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("LV_")}
+        env.update(extra, LIEVAE_HIP_LIB=path)
+        r = subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, pkg], env=env, check=True,
+                           capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    base = run({})
+    knobs = run({"LV_TILE_NSEG": "3", "LV_BWD_NSEG": "2", "LV_BWD_FGLOBAL": "1", "LV_TILE_WT": "0"})
+    assert (knobs != base) == honours
+    if not honours:
+        with open(path, "rb") as f:
+            assert b"LV_BWD_NSEG" not in f.read()

@@ -1,7 +1,8 @@
 import os, sys, json, subprocess
 res = {}
 for ns in [1, 2, 3, 4]:
-    env = dict(os.environ, LV_BWD_NSEG=str(ns))
+    env = dict(os.environ, LV_BWD_NSEG=str(ns),
+               LIEVAE_HIP_LIB=os.path.abspath("lie-vae_amd/lie_vae/liblievae_hip_ab.so"))  # knobs: A/B build only
     r = subprocess.run([sys.executable, "-c", """
 import sys, json, torch
 sys.path[:0] = ['lie-vae_amd', '.']

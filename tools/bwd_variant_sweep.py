@@ -1,7 +1,8 @@
 """A/B of backward tile-kernel builds (register budget) x degree-segment count.
 
 Each (library, nseg) runs in its own process: LIEVAE_HIP_LIB picks the build,
-LV_BWD_NSEG forces the segment count.  Prints us/call of lv_group_action_bwd at
+LV_BWD_NSEG forces the segment count (the libraries must be A/B builds, -DLV_AB_KNOBS:
+the product library reads no environment).  Prints us/call of lv_group_action_bwd at
 batch 4096, l = 10, C = 10 and a hash of (gang, gF) so that builds can be checked
 bit for bit against each other.
   python tools/bwd_variant_sweep.py lib1.so lib2.so ...

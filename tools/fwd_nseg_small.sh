@@ -3,6 +3,7 @@
 # us per launch of the config-2 fused forward (l = 10, C = 10, fp32).
 set -u
 cd "$(dirname "$0")/.."
+export LIEVAE_HIP_LIB="$PWD/lie-vae_amd/lie_vae/liblievae_hip_ab.so"  # the LV_* knobs exist only in the A/B build
 mkdir -p gpurun_out
 for B in 512 2048 4096; do
   for ns in 4 6 8; do

@@ -50,13 +50,21 @@ static int fslice(const ActionArgs& a, int nseg) {
 
 typedef void (*Kern)(ActionArgs);
 
+// Every launch is checked: a block larger than the kernel's __launch_bounds__ (or an LDS
+// request beyond the CU) fails to launch, and timing such "launches" measures nothing.
 static double timeit(Kern k, dim3 g, dim3 b, size_t lds, const ActionArgs& a, int reps) {
-  for (int w = 0; w < 20; ++w) hipLaunchKernelGGL(k, g, b, lds, 0, a);
+  for (int w = 0; w < 20; ++w) {
+    hipLaunchKernelGGL(k, g, b, lds, 0, a);
+    if (hipGetLastError() != hipSuccess) return -1.0;  // invalid configuration: no row
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, g, b, lds, 0, a);
+  for (int r = 0; r < reps; ++r) {
+    hipLaunchKernelGGL(k, g, b, lds, 0, a);
+    CK(hipGetLastError());
+  }
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -113,10 +121,12 @@ int main(int argc, char** argv) {
   const double bytes = (double)n * (12 + M * C * 4) + M * C * 4;
   const int gx = (int)((n + a.Sw - 1) / a.Sw);
 
-  for (int nw : {4, 5, 8, 12, 16}) {
+  // floor_kernel is __launch_bounds__(512): at most 8 waves per block
+  for (int nw : {4, 5, 8}) {
     const int gb = std::max(1, gx * 4 / nw);
     const double f0 = timeit(floor_kernel<0>, dim3(gb), dim3(64 * nw), 0, a, reps);
     const double f1 = timeit(floor_kernel<1>, dim3(gb), dim3(64 * nw), 0, a, reps);
+    if (f0 < 0 || f1 < 0) { printf("floor %d waves/block: launch failed\n", nw); continue; }
     printf("n=%lld floor %d waves/block x %d blocks: empty %.2f  loads %.2f us\n", (long long)n, nw, gb, f0, f1);
   }
   // reference + baseline: the library's tile kernel (C = 10 specialisation)

@@ -24,7 +24,8 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 600 python bench.py --sweep
+  step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
+  step bench 600 python bench.py --sweep 16384,65536,262144
   step bench_c5 600 python bench.py --lmax 20 --batch 8192 --dtype bf16 --no-cpu-baseline --steps 500
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline --multistream 1 --cold-launches 0 --no-fwd-bwd
