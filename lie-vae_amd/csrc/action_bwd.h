@@ -120,11 +120,6 @@ __device__ __forceinline__ float kdot(const float (&av)[2 * l + 1], const float 
   return acc;
 }
 
-// Upstream-gradient tile fill: global -> registers (16-byte loads, issued before the
-// prologue so their latency overlaps it) -> LDS.  Same head/body/tail split as
-// tile_flush; the LDS tile starts `mis` bytes past a 16-B boundary.
-constexpr int kBwdLoadsPerThread = 8;  // 16-B loads held in registers per thread
-
 // Up to l_max = kBwdWideMaxL the C = 10, one-group-per-block kernel fits 168 VGPRs
 // without spilling (156 at l = 10), so it has a twin built for 3 waves per SIMD
 // (WPE = 3) that the plan gives twice the segments: 26.9 -> 19.5 us per
@@ -214,21 +209,28 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     const int Sv = (int)min((int64_t)Sw, a.n - s0);
     const bool active = j < Sv;
     const int nbytes = Sv * (int)MC * 4;
-    // 1. upstream-gradient tile: issue the 16-byte loads first
+    // 1. upstream-gradient tile: global -> LDS by LDS-DMA (global_load_lds, 16-byte body,
+    //    4-byte head/tail), issued first thing.  No VGPR holds the tile in flight: the
+    //    register-staged form kept 32 VGPRs of loads live across the prologue, which the
+    //    3-waves-per-SIMD build spilled to scratch (96 B/lane; tools/bwdbench.hip: 13.5 ->
+    //    12.2 us at batch 4096, bitwise equal).
     const float* gsrc = a.gout + s0 * MC;
     const int mis = (int)(reinterpret_cast<uintptr_t>(gsrc) & 15);
     char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
-    const int head = min((16 - mis) & 15, nbytes);
-    const int nvec = (nbytes - head) >> 4;
-    const int tail0 = head + nvec * 16;
-    const __amdgpu_buffer_rsrc_t rg =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gsrc), 0, nbytes, kRawBufferFlags);
-    f4 gv[kBwdLoadsPerThread];
-#pragma unroll
-    for (int k = 0; k < kBwdLoadsPerThread; ++k) {
-      const int v = tid + k * nthr;
-      if (v < nvec)
-        gv[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rg, head + 16 * v, 0, 0));
+    {
+      const int head = min((16 - mis) & 15, nbytes);
+      const int nvec = (nbytes - head) >> 4;
+      const int tail0 = head + nvec * 16;
+      const char* gb = reinterpret_cast<const char*>(gsrc);
+      for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
+        if (v0 + lane < nvec)
+          __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(stage_b + head + 16 * v0),
+                                           16, 0, 0);
+      if (wave == 0) {
+        if (4 * lane < head) __builtin_amdgcn_global_load_lds(gsrc + lane, as_lds(stage_b), 4, 0, 0);
+        if (tail0 + 4 * lane < nbytes)
+          __builtin_amdgcn_global_load_lds(gb + tail0 + 4 * lane, as_lds(stage_b + tail0), 4, 0, 0);
+      }
     }
     // 2. prologue task (sample jt, slot q): sincos, multiples of slot q
     if (task) {
@@ -246,23 +248,8 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       }
       trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
     }
-    // 3. tile into LDS: the loaded body, the rest, head/tail elements
-#pragma unroll
-    for (int k = 0; k < kBwdLoadsPerThread; ++k) {
-      const int v = tid + k * nthr;
-      if (v < nvec) *reinterpret_cast<f4*>(stage_b + head + 16 * v) = gv[k];
-    }
-    for (int v = tid + kBwdLoadsPerThread * nthr; v < nvec; v += nthr)
-      *reinterpret_cast<f4*>(stage_b + head + 16 * v) =
-          __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rg, head + 16 * v, 0, 0));
-    {
-      const int nedge = head / 4 + (nbytes - tail0) / 4;
-      if (tid < nedge) {
-        const int b = tid < head / 4 ? tid * 4 : tail0 + (tid - head / 4) * 4;
-        *reinterpret_cast<float*>(stage_b + b) =
-            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, b, 0, 0));
-      }
-    }
+    // 3. the LDS-DMA writes of this wave have landed (an LDS-DMA is counted in vmcnt)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     block_sync_lds();
 
     float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
@@ -310,10 +297,25 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
           // the block's slab (groups in order)
           wave_lds_sync();
           const float* col0 = reinterpret_cast<const float*>(stage_b) + r0 * C;
-          for (int e = lane; e < nn * C; e += 64) {
-            float sum = col0[e];
-            for (int jj = 1; jj < Sv; ++jj) sum += col0[jj * MC + e];
-            slabL[r0 * C + e] += sum;
+          constexpr int kSw = CT > 0 ? 64 / CT : 1;
+          if (CT > 0 && Sv == kSw && Sw == kSw) {
+            // full group, compile-time size: the Sw loads of an element are issued
+            // together (one LDS round trip), summed in the same sample order
+            for (int e = lane; e < nn * C; e += 64) {
+              float v[kSw];
+#pragma unroll
+              for (int jj = 0; jj < kSw; ++jj) v[jj] = col0[jj * MC + e];
+              float sum = v[0];
+#pragma unroll
+              for (int jj = 1; jj < kSw; ++jj) sum += v[jj];
+              slabL[r0 * C + e] += sum;
+            }
+          } else {
+            for (int e = lane; e < nn * C; e += 64) {
+              float sum = col0[e];
+              for (int jj = 1; jj < Sv; ++jj) sum += col0[jj * MC + e];
+              slabL[r0 * C + e] += sum;
+            }
           }
         }
       }

@@ -68,4 +68,9 @@ __device__ __forceinline__ float dpp_swap_adjacent(float x) {
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// LDS pointer for __builtin_amdgcn_global_load_lds (global -> LDS DMA; the destination is
+// the wave-uniform base + lane * size).
+typedef __attribute__((address_space(3))) void* lds_vp;
+__device__ __forceinline__ lds_vp as_lds(const void* p) { return (lds_vp)(p); }
+
 }  // namespace lv

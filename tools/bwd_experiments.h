@@ -8,6 +8,9 @@
 //                 table, so no wave waits for another wave's loads or for wave 0's prologue
 //   kXSlabUnroll: the per-degree dF slab sum over the group's samples with the compile-
 //                 time group size (loads batched) when the group is full
+//   kXMultReg   : the X products generate their (cos, sin) multiples in registers from
+//                 the slot's (cos, sin) (read once per lane) instead of reading the LDS
+//                 table per product: 4 VALU per multiple against 2 LDS bytes... per lane
 //   kXGlds      : the upstream-gradient tile goes global -> LDS by LDS-DMA
 //                 (global_load_lds: 16-byte body, 4-byte edges; with kXWaveLocal 4-byte
 //                 runs of the wave's rows): no VGPRs (nor scratch) hold it in flight
@@ -20,10 +23,35 @@
 namespace lv {
 
 constexpr int kXWaveLocal = 1, kXSlabUnroll = 2, kXDiagNoG = 4, kXDiagNoSlab = 8,
-              kXDiagNoChain = 16, kXGlds = 32;
+              kXDiagNoChain = 16, kXGlds = 32, kXMultReg = 64;
 
-typedef __attribute__((address_space(3))) void* lds_vp;
-__device__ __forceinline__ lds_vp as_lds(const void* p) { return (lds_vp)(p); }
+// y = X x (T = false) or X^T x (T = true) with the multiples generated in registers by
+// trig_row_fill's recurrence from (cos, sin) of the slot's angle: bitwise equal to the
+// table version, no LDS reads (4 VALU per multiple instead).
+template <int l, bool T>
+__device__ __forceinline__ void xm_rec(float c1, float s1, const float (&x)[2 * l + 1],
+                                       float (&y)[2 * l + 1]) {
+  y[l] = x[l];
+  float cf = c1, sf = s1;
+  sfor<l>([&](auto F) {
+    constexpr int f = LV_CV(F) + 1;
+    if constexpr (f >= 2) {
+      const float cn = fmaf(cf, c1, -(sf * s1));
+      sf = fmaf(sf, c1, cf * s1);
+      cf = cn;
+    }
+    constexpr int i = l - f, i2 = l + f;  // rows with frequency +f and -f
+    if constexpr (!T) {
+      y[i] = fmaf(cf, x[i], sf * x[2 * l - i]);
+      y[i2] = fmaf(cf, x[i2], -(sf * x[2 * l - i2]));
+    } else {
+      y[i] = fmaf(cf, x[i], -(sf * x[2 * l - i]));
+      y[i2] = fmaf(cf, x[i2], sf * x[2 * l - i2]);
+    }
+  });
+}
+
+constexpr int kBwdLoadsPerThread = 8;  // register-staged tile: 16-B loads per thread
 
 __host__ __device__ inline int bwdx_trig_floats(int Sw, int L, int nseg, int var) {
   return (var & kXWaveLocal) ? nseg * bwd_trig_floats(Sw, L) : bwd_trig_floats(Sw, L);
@@ -202,6 +230,15 @@ void bwd_x_kernel(ActionBwdArgs a) {
   float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
   const float* tj = trig_w + min(j, Sw - 1) * kRow;
   float ga = 0.f, gb = 0.f, gc = 0.f;
+  float mc[3], ms[3];  // kXMultReg: (cos, sin) of the three slots, f = 1 of the table
+  if constexpr ((VAR & kXMultReg) != 0) {
+    constexpr int TP = TrigLds<LT>::TP;
+#pragma unroll
+    for (int A = 0; A < 3; ++A) {
+      mc[A] = tj[2 * A * TP + 1];
+      ms[A] = tj[(2 * A + 1) * TP + 1];
+    }
+  }
   sfor<LT + 1>([&](auto Lc) {
     constexpr int l = LV_CV(Lc);
     if (l >= lo && l < hi) {
@@ -209,22 +246,28 @@ void bwd_x_kernel(ActionBwdArgs a) {
       constexpr int r0 = l * l;
       if constexpr (!(VAR & kXDiagNoChain)) {
         float p2[nn], p4[nn], gq[nn], u[nn];
+        constexpr bool MR = (VAR & kXMultReg) != 0;
         {
           float f0[nn];
           sfor<nn>([&](auto K) { f0[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * C]; });
-          xm<l>(mult_lds<l, 2, LT>(tj), f0, u);
+          if constexpr (MR) xm_rec<l, false>(mc[2], ms[2], f0, u);
+          else xm<l>(mult_lds<l, 2, LT>(tj), f0, u);
         }
         jmul<l>(u, p2);
-        xm<l>(mult_lds<l, 1, LT>(tj), p2, u);
+        if constexpr (MR) xm_rec<l, false>(mc[1], ms[1], p2, u);
+        else xm<l>(mult_lds<l, 1, LT>(tj), p2, u);
         jmul<l>(u, p4);
         sfor<nn>([&](auto K) { gq[LV_CV(K)] = active ? tile_lane[(r0 + LV_CV(K)) * C] : 0.f; });
-        xm_t<l>(mult_lds<l, 0, LT>(tj), gq, u);
+        if constexpr (MR) xm_rec<l, true>(mc[0], ms[0], gq, u);
+        else xm_t<l>(mult_lds<l, 0, LT>(tj), gq, u);
         ga += kdot<l>(u, p4);
         jmul<l>(u, p4);
-        xm_t<l>(mult_lds<l, 1, LT>(tj), p4, u);
+        if constexpr (MR) xm_rec<l, true>(mc[1], ms[1], p4, u);
+        else xm_t<l>(mult_lds<l, 1, LT>(tj), p4, u);
         gb += kdot<l>(u, p2);
         jmul<l>(u, p2);
-        xm_t<l>(mult_lds<l, 2, LT>(tj), p2, u);
+        if constexpr (MR) xm_rec<l, true>(mc[2], ms[2], p2, u);
+        else xm_t<l>(mult_lds<l, 2, LT>(tj), p2, u);
         {
           float f0[nn];
           sfor<nn>([&](auto K) { f0[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * C]; });

@@ -153,6 +153,12 @@ int main(int argc, char** argv) {
     var(bwd_x_kernel<L, kXGlds | kXSlabUnroll>, kXGlds | kXSlabUnroll, "glds+unroll", true);
     var(bwd_x_kernel<L, kXGlds | kXWaveLocal | kXSlabUnroll>, kXGlds | kXWaveLocal | kXSlabUnroll,
         "glds wave-local+unroll", true);
+    constexpr int GU = kXGlds | kXSlabUnroll;
+    var(bwd_x_kernel<L, GU | kXMultReg>, GU | kXMultReg, "glds+unroll+multreg", true);
+    var(bwd_x_kernel<L, GU | kXDiagNoSlab>, GU | kXDiagNoSlab, "glds+unroll no slab", false);
+    var(bwd_x_kernel<L, GU | kXDiagNoChain>, GU | kXDiagNoChain, "glds+unroll no chain", false);
+    var(bwd_x_kernel<L, GU | kXMultReg | kXDiagNoSlab>, GU | kXMultReg | kXDiagNoSlab,
+        "glds+unroll+multreg no slab", false);
     var(bwd_x_kernel<L, kXDiagNoG>, kXDiagNoG, "diag no G", false);
     var(bwd_x_kernel<L, kXDiagNoSlab>, kXDiagNoSlab, "diag no slab", false);
     var(bwd_x_kernel<L, kXDiagNoChain>, kXDiagNoChain, "diag no chain", false);
