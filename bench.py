@@ -270,7 +270,7 @@ def main():
         torch.cuda.synchronize(dev)
         # the first replay of a fresh graph pays its one-time upload; every graph is
         # replayed once here, outside the timed region, whatever --warmup is
-        for g in [warm_graph] + list(dict.fromkeys(timed)):
+        for g in dict.fromkeys([warm_graph] + timed):
             g.replay()
         torch.cuda.synchronize(dev)
 
