@@ -60,6 +60,11 @@ def main():
                     help="run the two GEMM-shaped layers (decoder 1x1->4x4 ConvTranspose2d, "
                          "encoder 4x4->1x1 head) as addmm on hipBLASLt (on) or through MIOpen "
                          "(off); nets.GEMM_LAYERS")
+    ap.add_argument("--bn", choices=["miopen", "native"], default="miopen",
+                    help="BatchNorm2d kernels: MIOpen or PyTorch's native ones (nets.NATIVE_BN)")
+    ap.add_argument("--bias-grad", choices=["reduce", "gemv"], default="reduce",
+                    help="stride-2 ConvTranspose2d bias gradient: strided reduction or a "
+                         "ones-vector GEMM (nets.BIAS_GEMV)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd, bwd, all-reduce, clip, Adam) in a "
                          "hipGraph and time its replays")
@@ -95,6 +100,8 @@ def main():
     from lie_vae.experiments.train_dp import DPTrainer, param_count
     from lie_vae.experiments.vae import VAE
     nets.GEMM_LAYERS = args.conv_gemm == "on"
+    nets.NATIVE_BN = args.bn == "native"
+    nets.BIAS_GEMV = args.bias_grad == "gemv"
 
     torch.manual_seed(0)
     model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,
@@ -143,7 +150,7 @@ def main():
                        "params": param_count(model),
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
-                       "conv_gemm": args.conv_gemm,
+                       "conv_gemm": args.conv_gemm, "bn": args.bn, "bias_grad": args.bias_grad,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,

@@ -75,12 +75,74 @@ class GemmConv2d(nn.Conv2d):
         return y.view(B, self.out_channels, 1, 1)
 
 
+# A/B switches for the remaining memory-bound pieces of the conv stacks (bench_train.py
+# --bn / --bias-grad; read when a model is built):
+#   NATIVE_BN: BatchNorm2d through PyTorch's own batch-norm kernels instead of MIOpen's
+#   BIAS_GEMV: the stride-2 ConvTranspose2d bias gradient (a sum over N, H, W of the
+#              output gradient) as a ones-vector GEMM instead of a strided reduction
+NATIVE_BN = False
+BIAS_GEMV = False
+
+
+class NativeBatchNorm2d(nn.BatchNorm2d):
+    """BatchNorm2d evaluated by PyTorch's native kernels (MIOpen disabled for this op
+    only); same parameters, buffers and arithmetic definition."""
+
+    def forward(self, x):
+        prev = torch.backends.cudnn.enabled
+        torch.backends.cudnn.enabled = False
+        try:
+            return super().forward(x)
+        finally:
+            torch.backends.cudnn.enabled = prev
+
+
+class _BiasAdd(torch.autograd.Function):
+    """y + b[c] with the bias gradient sum_{n,h,w} g[n, c, h, w] as ones[1, NHW] @ G[NHW, C]
+    when G is channels-last (a GEMM on hipBLASLt), else a plain sum."""
+
+    @staticmethod
+    def forward(ctx, y, b):
+        ctx.bdt = b.dtype
+        return y + b.to(y.dtype).view(1, -1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        C = g.shape[1]
+        if _cl(g):
+            g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
+            ones = g2.new_ones(1, g2.shape[0])
+            gb = (ones @ g2).view(C)
+        else:
+            gb = g.sum((0, 2, 3))
+        return g, gb.to(ctx.bdt)
+
+
+class BiasGemvConvTranspose2d(nn.ConvTranspose2d):
+    """ConvTranspose2d whose bias is added by _BiasAdd (same parameters / state_dict)."""
+
+    def forward(self, x, output_size=None):
+        if self.bias is None or output_size is not None:
+            return super().forward(x, output_size)
+        y = torch.nn.functional.conv_transpose2d(x, self.weight, None, self.stride, self.padding,
+                                                 self.output_padding, self.groups, self.dilation)
+        return _BiasAdd.apply(y, self.bias)
+
+
 def _conv(*a):
     return (GemmConv2d if GEMM_LAYERS else nn.Conv2d)(*a)
 
 
 def _convt(*a):
     return (GemmConvTranspose2d if GEMM_LAYERS else nn.ConvTranspose2d)(*a)
+
+
+def _convt_s2(*a):
+    return (BiasGemvConvTranspose2d if BIAS_GEMV else nn.ConvTranspose2d)(*a)
+
+
+def _bn(c):
+    return (NativeBatchNorm2d if NATIVE_BN else nn.BatchNorm2d)(c)
 
 
 class View(nn.Module):
@@ -103,7 +165,7 @@ def _down_stack(in_dims, hidden, out_dims, batch_norm):
     for i, width in enumerate([hidden, hidden * 2, hidden * 4, hidden * 8]):
         layers.append(nn.Conv2d(c, width, 4, 2, 1))
         if batch_norm:
-            layers.append(nn.BatchNorm2d(width))
+            layers.append(_bn(width))
         layers.append(nn.LeakyReLU(0.2, inplace=True))
         c = width
     layers += [_conv(c, out_dims, 4, 1, 0), Flatten()]
@@ -130,8 +192,8 @@ class DeconvNet(nn.Sequential):
     def __init__(self, in_dims, hidden_dims, rgb=False):
         layers = [View(-1, in_dims, 1, 1), _convt(in_dims, hidden_dims, 4, 1, 0), nn.ReLU()]
         for _ in range(3):
-            layers += [nn.ConvTranspose2d(hidden_dims, hidden_dims, 4, 2, 1), nn.ReLU()]
-        layers.append(nn.ConvTranspose2d(hidden_dims, 3 if rgb else 1, 4, 2, 1))
+            layers += [_convt_s2(hidden_dims, hidden_dims, 4, 2, 1), nn.ReLU()]
+        layers.append(_convt_s2(hidden_dims, 3 if rgb else 1, 4, 2, 1))
         super().__init__(*layers)
 
 

@@ -27,11 +27,17 @@ for v in $VARIANTS; do
     bf16) A="--amp bf16 --channels-last" ;;
     f32_nogemm) A="--conv-gemm off" ;;
     bf16_nogemm) A="--amp bf16 --channels-last --conv-gemm off" ;;
+    bf16_nbn) A="--amp bf16 --channels-last --bn native" ;;
+    bf16_gemv) A="--amp bf16 --channels-last --bias-grad gemv" ;;
+    bf16_both) A="--amp bf16 --channels-last --bn native --bias-grad gemv" ;;
+    f32_nbn) A="--bn native" ;;
+    f32_both) A="--bn native --bias-grad gemv" ;;
     *) echo "unknown variant $v"; exit 2 ;;
   esac
   step warm_$v 600 python bench_train.py --steps 3 --warmup 2 $A
   step time_$v 300 python bench_train.py --steps 30 --warmup 5 $A
   step timedb_$v 300 python bench_train.py --steps 30 --warmup 5 --no-find $A
+  if [ "${TIMEONLY:-0}" = 1 ]; then continue; fi
   ( cd /tmp && export TMPDIR=/tmp )
   export TMPDIR=/tmp
   # 3 warm-up + 1 FLOP-count + 20 timed steps
