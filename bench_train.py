@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--bias-grad", choices=["reduce", "gemv"], default="reduce",
                     help="stride-2 ConvTranspose2d bias gradient: strided reduction or a "
                          "ones-vector GEMM (nets.BIAS_GEMV)")
+    ap.add_argument("--deconv", choices=["transposed", "phase"], default="transposed",
+                    help="stride-2 ConvTranspose2d as MIOpen's transposed convolution or as one "
+                         "3x3 convolution + pixel shuffle (nets.PHASE_DECONV)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd, bwd, all-reduce, clip, Adam) in a "
                          "hipGraph and time its replays")
@@ -102,6 +105,7 @@ def main():
     nets.GEMM_LAYERS = args.conv_gemm == "on"
     nets.NATIVE_BN = args.bn == "native"
     nets.BIAS_GEMV = args.bias_grad == "gemv"
+    nets.PHASE_DECONV = args.deconv == "phase"
 
     torch.manual_seed(0)
     model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,
@@ -151,6 +155,7 @@ def main():
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
                        "conv_gemm": args.conv_gemm, "bn": args.bn, "bias_grad": args.bias_grad,
+                       "deconv": args.deconv,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,

@@ -256,7 +256,9 @@ __device__ __forceinline__ void tile_flush_rt(OutT* gout, const char* stage_b, i
 // instead (no global store precedes the flush, so these loads never wait behind stores);
 // that costs ~10 cycles of address processing per wave load instruction, which is why
 // the C = 10 path keeps it in LDS (l = 20 bf16: 18.5 -> 5 us of skeleton, tools/c5bench).
-template <int LT, int CT, bool FUSED, typename OutT>
+// MREG: the X products generate their multiples in registers (xrot_rec) from the slot's
+// (cos, sin) instead of reading them from the LDS table (A/B, tools/fwdbench.hip).
+template <int LT, int CT, bool FUSED, typename OutT, bool MREG = false>
 __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kRow = TrigLds<LT>::kRow;
@@ -341,6 +343,15 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   const float* Fl = FG ? a.F + c : (CT > 0 ? Fall + c : Fw + c * frows - rows_lo);
   const int fstep = (FG || CT > 0) ? C : 1;  // stride between consecutive rows of a column
 
+  float mc[3], ms[3];  // MREG: (cos, sin) of the three slots (f = 1 of the table)
+  if constexpr (MREG) {
+    constexpr int TP = TrigLds<LT>::TP;
+#pragma unroll
+    for (int A = 0; A < 3; ++A) {
+      mc[A] = tj[2 * A * TP + 1];
+      ms[A] = tj[(2 * A + 1) * TP + 1];
+    }
+  }
   sfor<LT + 1>([&](auto Lc) {
     constexpr int l = LV_CV(Lc);
     if (l >= lo && l < hi) {
@@ -348,11 +359,19 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
       constexpr int r0 = l * l;
       float x[nn], y[nn];
       sfor<nn>([&](auto K) { x[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * fstep]; });
-      xrot_lds<l, 2, LT>(tj, x, y);
-      jmul<l>(y, x);
-      xrot_lds<l, 1, LT>(tj, x, y);
-      jmul<l>(y, x);
-      xrot_lds<l, 0, LT>(tj, x, y);
+      if constexpr (MREG && l >= 1) {
+        xrot_rec<l, false>(mc[2], ms[2], x, y);
+        jmul<l>(y, x);
+        xrot_rec<l, false>(mc[1], ms[1], x, y);
+        jmul<l>(y, x);
+        xrot_rec<l, false>(mc[0], ms[0], x, y);
+      } else {
+        xrot_lds<l, 2, LT>(tj, x, y);
+        jmul<l>(y, x);
+        xrot_lds<l, 1, LT>(tj, x, y);
+        jmul<l>(y, x);
+        xrot_lds<l, 0, LT>(tj, x, y);
+      }
       if (active) {
         OutT* d = st_lane + r0 * C;
         sfor<nn>([&](auto I) {

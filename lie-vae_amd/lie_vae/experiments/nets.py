@@ -129,6 +129,50 @@ class BiasGemvConvTranspose2d(nn.ConvTranspose2d):
         return _BiasAdd.apply(y, self.bias)
 
 
+PHASE_DECONV = False
+
+
+class PhaseConvTranspose2d(nn.ConvTranspose2d):
+    """ConvTranspose2d(c_in, c_out, 4, 2, 1) as ONE stride-1 3x3 convolution to 4·c_out
+    channels followed by a pixel shuffle (sub-pixel decomposition): output pixel
+    (2a + r, 2b + s) only sees inputs (a + di, b + dj), di in {r - 1, r}, through kernel tap
+    (3 - 2i + r, 3 - 2j + s) with i = di + 1, so phase (r, s) is a 2x2 sub-kernel of a
+    3x3 window.  The four phases become one forward convolution (an implicit GEMM that
+    MIOpen runs on MFMA) instead of a transposed (backward-data) convolution; the zero
+    taps cost 9/4 of the FLOPs.  Same parameters / state_dict; other shapes fall back."""
+
+    _IDX = {}
+
+    def _phase_ok(self):
+        return (self.kernel_size == (4, 4) and self.stride == (2, 2) and self.padding == (1, 1)
+                and self.output_padding == (0, 0) and self.dilation == (1, 1) and self.groups == 1)
+
+    def _w3(self):
+        dev = self.weight.device
+        if dev not in self._IDX:
+            k = torch.full((2, 3), 4, dtype=torch.long)
+            for r in range(2):
+                for i in range(3):
+                    if i - r in (0, 1):
+                        k[r, i] = 3 - 2 * i + r
+            self._IDX[dev] = k.to(dev)
+        k = self._IDX[dev]
+        w = torch.nn.functional.pad(self.weight, (0, 1, 0, 1))            # (cin, cout, 5, 5)
+        w = w[:, :, k[:, None, :, None], k[None, :, None, :]]            # (cin, cout, r, s, i, j)
+        cin, cout = self.in_channels, self.out_channels
+        return w.permute(1, 2, 3, 0, 4, 5).reshape(4 * cout, cin, 3, 3)
+
+    def forward(self, x, output_size=None):
+        if output_size is not None or not self._phase_ok():
+            return super().forward(x, output_size)
+        w3 = self._w3()
+        if _cl(self.weight):
+            w3 = w3.contiguous(memory_format=torch.channels_last)
+        b3 = self.bias.repeat_interleave(4) if self.bias is not None else None
+        y = torch.nn.functional.conv2d(x, w3, b3, 1, 1)
+        return torch.nn.functional.pixel_shuffle(y, 2)
+
+
 def _conv(*a):
     return (GemmConv2d if GEMM_LAYERS else nn.Conv2d)(*a)
 
@@ -138,6 +182,8 @@ def _convt(*a):
 
 
 def _convt_s2(*a):
+    if PHASE_DECONV:
+        return PhaseConvTranspose2d(*a)
     return (BiasGemvConvTranspose2d if BIAS_GEMV else nn.ConvTranspose2d)(*a)
 
 

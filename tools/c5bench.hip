@@ -42,18 +42,30 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(F, hF.data(), M * C * 4, hipMemcpyHostToDevice));
   const int gx = (int)((n + 5) / 6);
   std::vector<unsigned short> ref((size_t)n * M * C), got((size_t)n * M * C);
-  for (int nseg : {4, 8}) {
+  for (int nseg : {5, 6, 8}) {
     ActionArgs a{};
     a.v = v; a.F = F; a.out = out; a.n = n; a.MC = M * C; a.C = C; a.Sw = 6; a.write_through = 0;
     // equal-ish segments by cost: split degrees so sum (2 nnz + 12 l) balances (rough)
     const int cuts8[9] = {0, 8, 11, 13, 15, 16, 18, 19, 21};
-    const int cuts4[5] = {0, 11, 15, 18, 21};
-    for (int k = 0; k <= nseg; ++k) a.seg_lo[k] = nseg == 8 ? cuts8[k] : cuts4[k];
+    const int cuts6[7] = {0, 10, 13, 15, 17, 19, 21};
+    const int cuts5[6] = {0, 11, 14, 17, 19, 21};
+    for (int k = 0; k <= nseg; ++k) a.seg_lo[k] = nseg == 8 ? cuts8[k] : (nseg == 6 ? cuts6[k] : cuts5[k]);
     const size_t lds = tile_stage_bytes(6, a.MC, 2) + 4 * (size_t)6 * TrigLds<L>::kRow;
     const size_t lds_lib = lds + 4 * (size_t)a.MC;  // the library kernel stages the whole F
     const dim3 g(gx), b(64 * nseg);
     double lib = timeit(action_fwd_tile_kernel<L, C, true, __hip_bfloat16>, g, b, lds_lib, a, reps);
     CK(hipMemcpy(ref.data(), out, ref.size() * 2, hipMemcpyDeviceToHost));
+    {
+      Kern km = action_fwd_tile_kernel<L, C, true, __hip_bfloat16, true>;
+      CK(hipMemset(out, 0xff, ref.size() * 2));
+      hipLaunchKernelGGL(km, g, b, lds_lib, 0, a);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), out, got.size() * 2, hipMemcpyDeviceToHost));
+      const double tm = timeit(km, g, b, lds_lib, a, reps);
+      printf("nseg=%d library %.2f us | multiples in registers (MREG) %.2f us %s\n", nseg, lib, tm,
+             memcmp(ref.data(), got.data(), ref.size() * 2) ? "MISMATCH" : "bitwise-ok");
+    }
+    if (argc > 3) continue;  // MREG A/B only
     CK(hipMemset(out, 0xff, ref.size() * 2));
     hipLaunchKernelGGL(c5_persist_kernel<L>, dim3(std::min(512, gx)), b, lds, 0, a);
     CK(hipDeviceSynchronize());

@@ -31,6 +31,8 @@ for v in $VARIANTS; do
     bf16_gemv) A="--amp bf16 --channels-last --bias-grad gemv" ;;
     bf16_both) A="--amp bf16 --channels-last --bn native --bias-grad gemv" ;;
     f32_nbn) A="--bn native" ;;
+    bf16_phase) A="--amp bf16 --channels-last --bn native --deconv phase" ;;
+    f32_phase) A="--bn native --deconv phase" ;;
     f32_both) A="--bn native --bias-grad gemv" ;;
     *) echo "unknown variant $v"; exit 2 ;;
   esac
