@@ -183,12 +183,13 @@ struct LaneIn {
   float mu[9];
 };
 
-template <bool FUSED>
+// MAYMU = false: the caller guarantees a.mu == nullptr (compiled without the mu path).
+template <bool FUSED, bool MAYMU = true>
 __device__ __forceinline__ void lane_load(const ActionArgs& a, int64_t s, LaneIn& in) {
   if constexpr (FUSED) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) in.v[i] = a.v[s * 3 + i];
-    if (a.mu) {
+    if (MAYMU && a.mu) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) in.mu[i] = a.mu[s * 9 + i];
     }
@@ -200,14 +201,14 @@ __device__ __forceinline__ void lane_load(const ActionArgs& a, int64_t s, LaneIn
 
 // (cos, sin) of the three chain angles.  For transpose (D^T = X(-c) J X(-b) J X(-a)) the
 // slots are swapped and the sines negated.
-template <bool FUSED>
+template <bool FUSED, bool MAYMU = true>
 __device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& in, int64_t s,
                                             bool active, int c, bool write_ang, float c1[3],
                                             float s1[3]) {
   float cc[3], ss[3];
   if constexpr (FUSED) {
     float q[4];
-    if (a.mu) {
+    if (MAYMU && a.mu) {
       mu_exp_to_zyz_trig(in.mu, in.v, cc, ss, q);
     } else {
       exp_to_zyz_trig(in.v, cc, ss, q);

@@ -258,8 +258,9 @@ __device__ __forceinline__ void tile_flush_rt(OutT* gout, const char* stage_b, i
 // the C = 10 path keeps it in LDS (l = 20 bf16: 18.5 -> 5 us of skeleton, tools/c5bench).
 // MREG: the X products generate their multiples in registers (xrot_rec) from the slot's
 // (cos, sin) instead of reading them from the LDS table (A/B, tools/fwdbench.hip).
-template <int LT, int CT, bool FUSED, typename OutT, bool MREG = false>
-__global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
+// MAYMU = false: compiled without the mean-rotation (mu) prologue (a.mu must be null).
+template <int LT, int CT, bool FUSED, typename OutT, bool MREG = false, bool MAYMU = true>
+__device__ __forceinline__ void fwd_tile_body(const ActionArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kRow = TrigLds<LT>::kRow;
   constexpr bool FG = CT == 0 && LT >= kTileFGlobalMinL;  // spectrum from global, no LDS
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
   const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
   LaneIn in;
-  if (task) lane_load<FUSED>(a, st, in);
+  if (task) lane_load<FUSED, MAYMU>(a, st, in);
   // 2. this wave's spectrum slice: loads now, LDS writes after the prologue maths
   constexpr int kFPer = FG ? 1 : 6;
   float fv[kFPer];
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   }
   if (task) {
     float c1[3], s1[3];
-    lane_angles<FUSED>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
+    lane_angles<FUSED, MAYMU>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
     trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
   }
   if constexpr (FG) {
@@ -383,6 +384,11 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   });
   block_sync_lds();
   tile_flush_rt<OutT>(gout, stage_b, mis, Sv * (int)MC * (int)sizeof(OutT), a.write_through);
+}
+
+template <int LT, int CT, bool FUSED, typename OutT, bool MREG = false>
+__global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
+  fwd_tile_body<LT, CT, FUSED, OutT, MREG>(a);
 }
 
 // ------------------------------------------------------------ Wigner-D blocks

@@ -189,4 +189,9 @@ __global__ __launch_bounds__(512) void c5_floor_kernel(ActionArgs a) {
     if (lds[threadIdx.x & 63] == 1234.5f) reinterpret_cast<float*>(a.out)[threadIdx.x] = 1.f;
   }
 }
+template <int LT>
+__global__ __launch_bounds__(512) void c5_nomu_kernel(ActionArgs a) {
+  fwd_tile_body<LT, 10, true, __hip_bfloat16, false, false>(a);
+}
+
 }  // namespace lv

@@ -64,6 +64,13 @@ int main(int argc, char** argv) {
       const double tm = timeit(km, g, b, lds_lib, a, reps);
       printf("nseg=%d library %.2f us | multiples in registers (MREG) %.2f us %s\n", nseg, lib, tm,
              memcmp(ref.data(), got.data(), ref.size() * 2) ? "MISMATCH" : "bitwise-ok");
+      Kern kn = c5_nomu_kernel<L>;
+      CK(hipMemset(out, 0xff, ref.size() * 2));
+      hipLaunchKernelGGL(kn, g, b, lds_lib, 0, a);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), out, got.size() * 2, hipMemcpyDeviceToHost));
+      printf("nseg=%d no-mu build %.2f us %s\n", nseg, timeit(kn, g, b, lds_lib, a, reps),
+             memcmp(ref.data(), got.data(), ref.size() * 2) ? "MISMATCH" : "bitwise-ok");
     }
     if (argc > 3) continue;  // MREG A/B only
     CK(hipMemset(out, 0xff, ref.size() * 2));

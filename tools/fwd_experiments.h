@@ -798,4 +798,17 @@ __global__ __launch_bounds__(512) void tile6_kernel(ActionArgs a) {
   block_sync_lds();
   flush_rows<float, POL>(gout, stage_b, Sv, MC, L1 * L1 * C, MC, tid, (int)blockDim.x);
 }
+// Occupancy / prologue variants of the library tile kernel (same body, fwd_tile_body):
+//   nomu: compiled without the mean-rotation (fp64) prologue path (a.mu == null)
+//   w8  : register budget for 8 waves per SIMD (64 VGPRs), so 5 blocks of 6 waves fit a CU
+template <int LT, int CT, bool MAYMU>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8)))
+void tile_w8_kernel(ActionArgs a) {
+  fwd_tile_body<LT, CT, true, float, false, MAYMU>(a);
+}
+template <int LT, int CT>
+__global__ __launch_bounds__(512) void tile_nomu_kernel(ActionArgs a) {
+  fwd_tile_body<LT, CT, true, float, false, false>(a);
+}
+
 }  // namespace lv

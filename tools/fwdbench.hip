@@ -166,6 +166,25 @@ int main(int argc, char** argv) {
   for (int nseg : {4, 5, 6, 7, 8})
     printf("n=%lld lib tile nseg=%d: %s %8.2f us  | multiples in registers (MREG) %8.2f us\n", (long long)n, nseg,
            wt ? "sc1" : "nt", lib_tile(nseg, wt, false), lib_tile(nseg, wt, false, 0, true));
+  auto occ = [&](Kern k, int nseg) {
+    ActionArgs b = a;
+    plan(nseg, 60.0, b.seg_lo);
+    b.fpitch = fslice(b, nseg);
+    b.write_through = wt;
+    const size_t lds = tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)b.Sw * TrigLds<L>::kRow);
+    const size_t bad = check(k, dim3(gx), dim3(64 * nseg), lds, b, n, ref);
+    const double t = timeit(k, dim3(gx), dim3(64 * nseg), lds, b, reps);
+    return std::make_pair(t, bad);
+  };
+  for (int nseg : {4, 5, 6}) {
+    auto a0 = occ(action_fwd_tile_kernel<L, C, true, float>, nseg);
+    auto a1 = occ(tile_nomu_kernel<L, C>, nseg);
+    auto a2 = occ(tile_w8_kernel<L, C, true>, nseg);
+    auto a3 = occ(tile_w8_kernel<L, C, false>, nseg);
+    printf("n=%lld nseg=%d: lib %7.2f | nomu %7.2f%s | w8 %7.2f%s | nomu+w8 %7.2f%s us\n", (long long)n, nseg,
+           a0.first, a1.first, a1.second ? " DIFF" : "", a2.first, a2.second ? " DIFF" : "", a3.first,
+           a3.second ? " DIFF" : "");
+  }
   if (!(argc > 3 && std::string(argv[3]) == "twophase")) return 0;
   // two-phase tile kernel: degrees [0, L1) then [L1, L], the first part's rows written
   // while the second part computes
