@@ -60,8 +60,9 @@ def main():
                     help="run the two GEMM-shaped layers (decoder 1x1->4x4 ConvTranspose2d, "
                          "encoder 4x4->1x1 head) as addmm on hipBLASLt (on) or through MIOpen "
                          "(off); nets.GEMM_LAYERS")
-    ap.add_argument("--bn", choices=["miopen", "native"], default="miopen",
-                    help="BatchNorm2d kernels: MIOpen or PyTorch's native ones (nets.NATIVE_BN)")
+    ap.add_argument("--bn", choices=["miopen", "native"], default="native",
+                    help="BatchNorm2d on channels-last inputs: PyTorch's native NHWC kernels "
+                         "(default) or MIOpen (nets.NATIVE_BN); NCHW always takes MIOpen")
     ap.add_argument("--bias-grad", choices=["reduce", "gemv"], default="reduce",
                     help="stride-2 ConvTranspose2d bias gradient: strided reduction or a "
                          "ones-vector GEMM (nets.BIAS_GEMV)")

@@ -75,20 +75,25 @@ class GemmConv2d(nn.Conv2d):
         return y.view(B, self.out_channels, 1, 1)
 
 
-# A/B switches for the remaining memory-bound pieces of the conv stacks (bench_train.py
-# --bn / --bias-grad; read when a model is built):
-#   NATIVE_BN: BatchNorm2d through PyTorch's own batch-norm kernels instead of MIOpen's
-#   BIAS_GEMV: the stride-2 ConvTranspose2d bias gradient (a sum over N, H, W of the
-#              output gradient) as a ones-vector GEMM instead of a strided reduction
-NATIVE_BN = False
+# Switches for the memory-bound pieces of the conv stacks (bench_train.py --bn /
+# --bias-grad / --deconv; read when a model is built).  Measured on MI355X, config 3
+# (B = 512, steady state, profiles/r03_train_ab.txt):
+#   NATIVE_BN: BatchNorm2d on channels-last inputs through PyTorch's native NHWC kernels
+#              instead of MIOpen's (bf16 NHWC step 7.66 -> 7.41 ms); NCHW inputs keep
+#              MIOpen, which is faster there (f32 NCHW 14.2 vs 15.2 ms with native)
+#   BIAS_GEMV: the stride-2 ConvTranspose2d bias gradient as a ones-vector GEMM (off:
+#              10.0 vs 7.7 ms -- without its bias MIOpen picks slower deconv solutions)
+NATIVE_BN = True
 BIAS_GEMV = False
 
 
 class NativeBatchNorm2d(nn.BatchNorm2d):
-    """BatchNorm2d evaluated by PyTorch's native kernels (MIOpen disabled for this op
-    only); same parameters, buffers and arithmetic definition."""
+    """BatchNorm2d evaluated by PyTorch's native kernels for channels-last inputs (MIOpen
+    disabled for this op only); same parameters, buffers and arithmetic definition."""
 
     def forward(self, x):
+        if not _cl(x):
+            return super().forward(x)
         prev = torch.backends.cudnn.enabled
         torch.backends.cudnn.enabled = False
         try:
@@ -129,7 +134,7 @@ class BiasGemvConvTranspose2d(nn.ConvTranspose2d):
         return _BiasAdd.apply(y, self.bias)
 
 
-PHASE_DECONV = False
+PHASE_DECONV = False  # off: 10.5 vs 7.4 ms (bf16), 22.1 vs 15.2 ms (f32)
 
 
 class PhaseConvTranspose2d(nn.ConvTranspose2d):
