@@ -144,33 +144,6 @@ __device__ __forceinline__ void xrot_lds(const float* tj, const float (&x)[2 * l
   });
 }
 
-// y = X_l(θ) x (T = false) or X_l(θ)^T x (T = true) with the multiples generated in
-// registers by trig_row_fill's recurrence from (cos θ, sin θ): bitwise equal to xrot /
-// xrot_lds / xrot_t on a table filled by trig_row_fill, with no table reads (4 VALU per
-// multiple instead of the LDS traffic of a (cos, sin) table row).
-template <int l, bool T>
-__device__ __forceinline__ void xrot_rec(float c1, float s1, const float (&x)[2 * l + 1],
-                                         float (&y)[2 * l + 1]) {
-  y[l] = x[l];
-  float cf = c1, sf = s1;
-  sfor<l>([&](auto F) {
-    constexpr int f = LV_CV(F) + 1;
-    if constexpr (f >= 2) {
-      const float cn = fmaf(cf, c1, -(sf * s1));
-      sf = fmaf(sf, c1, cf * s1);
-      cf = cn;
-    }
-    constexpr int i = l - f, i2 = l + f;  // the rows of frequency +f and -f
-    if constexpr (!T) {
-      y[i] = fmaf(cf, x[i], sf * x[2 * l - i]);
-      y[i2] = fmaf(cf, x[i2], -(sf * x[2 * l - i2]));
-    } else {
-      y[i] = fmaf(cf, x[i], -(sf * x[2 * l - i]));
-      y[i2] = fmaf(cf, x[i2], sf * x[2 * l - i2]);
-    }
-  });
-}
-
 // y = X_l(θ_A)^T x = X_l(-θ_A) x
 template <int l, int A, int LT>
 __device__ __forceinline__ void xrot_t(const TrigTab<LT>& t, const float (&x)[2 * l + 1],

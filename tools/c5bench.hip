@@ -56,23 +56,46 @@ int main(int argc, char** argv) {
     double lib = timeit(action_fwd_tile_kernel<L, C, true, __hip_bfloat16>, g, b, lds_lib, a, reps);
     CK(hipMemcpy(ref.data(), out, ref.size() * 2, hipMemcpyDeviceToHost));
     {
-      Kern km = action_fwd_tile_kernel<L, C, true, __hip_bfloat16, true>;
-      CK(hipMemset(out, 0xff, ref.size() * 2));
-      hipLaunchKernelGGL(km, g, b, lds_lib, 0, a);
-      CK(hipDeviceSynchronize());
-      CK(hipMemcpy(got.data(), out, got.size() * 2, hipMemcpyDeviceToHost));
-      const double tm = timeit(km, g, b, lds_lib, a, reps);
-      printf("nseg=%d library %.2f us | multiples in registers (MREG) %.2f us %s\n", nseg, lib, tm,
-             memcmp(ref.data(), got.data(), ref.size() * 2) ? "MISMATCH" : "bitwise-ok");
       Kern kn = c5_nomu_kernel<L>;
       CK(hipMemset(out, 0xff, ref.size() * 2));
       hipLaunchKernelGGL(kn, g, b, lds_lib, 0, a);
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(got.data(), out, got.size() * 2, hipMemcpyDeviceToHost));
-      printf("nseg=%d no-mu build %.2f us %s\n", nseg, timeit(kn, g, b, lds_lib, a, reps),
+      printf("nseg=%d library %.2f us | no-mu build %.2f us %s\n", nseg, lib, timeit(kn, g, b, lds_lib, a, reps),
              memcmp(ref.data(), got.data(), ref.size() * 2) ? "MISMATCH" : "bitwise-ok");
     }
-    if (argc > 3) continue;  // MREG A/B only
+    // two-phase tile kernel: degrees [0, L1) then [L1, L], nw waves, one segment per phase each
+    for (int L1 : {14, 15, 16})
+      for (int nw : {5, 6, 7}) {
+        if (L + 1 - L1 < nw) continue;
+        ActionArgs t = a;
+        auto cost = [](int l) { return (2.0 * l + 1) * (2.0 * l + 1) / 2 + 6.0 * (2 * l + 1) + 20; };
+        auto split = [&](int lo, int hi, int k, int* seg) {  // greedy equal-cost split
+          double tot = 0; for (int l = lo; l < hi; ++l) tot += cost(l);
+          int m = 0; double acc = 0; seg[0] = lo;
+          for (int l = lo; l < hi && m < k - 1; ++l) {
+            acc += cost(l);
+            if (acc >= tot * (m + 1) / k || hi - (l + 1) == k - 1 - m) seg[++m] = l + 1;
+          }
+          while (m < k - 1) { seg[m + 1] = seg[m] + 1; ++m; }
+          seg[k] = hi;
+        };
+        split(0, L1, nw, t.seg_lo);
+        split(L1, L + 1, nw, t.seg_lo + nw + 1);
+        const int P = tile2_pitch(M, L1 * L1, C, 2);
+        const size_t l2 = (size_t)6 * P + 4 * ((size_t)6 * TrigLds<L>::kRow + (size_t)M * C);
+        Kern k2 = action_fwd_tile2_kernel<L, true, __hip_bfloat16>;
+        CK(hipMemset(out, 0xff, ref.size() * 2));
+        hipLaunchKernelGGL(k2, dim3(gx), dim3(64 * nw), l2, 0, t);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), out, got.size() * 2, hipMemcpyDeviceToHost));
+        const bool ok = !memcmp(ref.data(), got.data(), ref.size() * 2);
+        printf("   two-phase L1=%d waves=%d lds=%zu: capped %.2f us, uncapped %.2f us %s\n", L1, nw, l2,
+               timeit(k2, dim3(gx), dim3(64 * nw), l2, t, reps),
+               timeit(c5_tile2_free_kernel<L>, dim3(gx), dim3(64 * nw), l2, t, reps), ok ? "bitwise-ok" : "MISMATCH");
+      }
+    if (argc > 3) continue;  // A/B rows only
     CK(hipMemset(out, 0xff, ref.size() * 2));
     hipLaunchKernelGGL(c5_persist_kernel<L>, dim3(std::min(512, gx)), b, lds, 0, a);
     CK(hipDeviceSynchronize());

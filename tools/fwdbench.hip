@@ -131,17 +131,13 @@ int main(int argc, char** argv) {
   }
   // reference + baseline: the library's tile kernel (C = 10 specialisation)
   std::vector<float> ref((size_t)n * M * C);
-  auto lib_tile = [&](int nseg, int wt, bool keep, size_t pad = 0, bool mreg = false) {
+  auto lib_tile = [&](int nseg, int wt, bool keep, size_t pad = 0) {
     ActionArgs b = a;
     plan(nseg, 60.0, b.seg_lo);
     b.fpitch = fslice(b, nseg);
     b.write_through = wt;
     const size_t lds = pad + tile_stage_bytes(b.Sw, b.MC, 4) + 4 * ((size_t)b.Sw * TrigLds<L>::kRow);  // spectrum in the tile
-    Kern k = mreg ? action_fwd_tile_kernel<L, C, true, float, true> : action_fwd_tile_kernel<L, C, true, float>;
-    if (mreg) {
-      const size_t bad = check(k, dim3(gx), dim3(64 * nseg), lds, b, n, ref);
-      if (bad) printf("   MREG nseg=%d: %zu elements differ from the library\n", nseg, bad);
-    }
+    Kern k = action_fwd_tile_kernel<L, C, true, float>;
     if (keep) {
       hipLaunchKernelGGL(k, dim3(gx), dim3(64 * nseg), lds, 0, b);
       CK(hipDeviceSynchronize());
@@ -164,8 +160,7 @@ int main(int argc, char** argv) {
   }
   const int wt = n * M * C * 4 <= (24ll << 20) ? 1 : 0;  // the library's store policy
   for (int nseg : {4, 5, 6, 7, 8})
-    printf("n=%lld lib tile nseg=%d: %s %8.2f us  | multiples in registers (MREG) %8.2f us\n", (long long)n, nseg,
-           wt ? "sc1" : "nt", lib_tile(nseg, wt, false), lib_tile(nseg, wt, false, 0, true));
+    printf("n=%lld lib tile nseg=%d: %s %8.2f us\n", (long long)n, nseg, wt ? "sc1" : "nt", lib_tile(nseg, wt, false));
   auto occ = [&](Kern k, int nseg) {
     ActionArgs b = a;
     plan(nseg, 60.0, b.seg_lo);
