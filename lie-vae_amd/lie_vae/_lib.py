@@ -98,9 +98,16 @@ def last_error():
     return load().lv_last_error().decode(errors="replace")
 
 
+_fns = {}
+
+
 def call(name, *args):
-    """Invoke an entry point; non-zero return -> LieVaeHipError with the library message."""
-    rc = getattr(load(), name)(*args)
+    """Invoke an entry point; non-zero return -> LieVaeHipError with the library message.
+    (Bound functions are looked up once; pointers and the stream travel as plain ints.)"""
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(load(), name)
+    rc = fn(*args)
     if rc != 0:
         raise LieVaeHipError(f"{name} failed ({rc}): {last_error()}")
 
@@ -120,11 +127,12 @@ def plan(kind, *args):
 
 
 def stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The caller's current HIP stream (raw handle, as an int)."""
+    return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device())
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    return t.data_ptr() if t is not None else None
 
 
 def require_device(*tensors):

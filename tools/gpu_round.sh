@@ -30,6 +30,8 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 50 --no-cpu-baseline --multistream 1 --cold-launches 0 --no-fwd-bwd
   rm -f "$OUT"/prof/*kernel_trace.csv
+  step rocprof_driver 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_driver" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+  rm -f "$OUT"/prof_driver/*kernel_trace.csv
 fi
 if [ "$MODE" = all ] || [ "$MODE" = train ]; then
   step train_c3 600 python bench_train.py --global-batch 512 --steps 20
