@@ -66,9 +66,10 @@ def main():
     ap.add_argument("--bias-grad", choices=["reduce", "gemv"], default="reduce",
                     help="stride-2 ConvTranspose2d bias gradient: strided reduction or a "
                          "ones-vector GEMM (nets.BIAS_GEMV)")
-    ap.add_argument("--deconv", choices=["transposed", "phase"], default="transposed",
-                    help="stride-2 ConvTranspose2d as MIOpen's transposed convolution or as one "
-                         "3x3 convolution + pixel shuffle (nets.PHASE_DECONV)")
+    ap.add_argument("--deconv", choices=["transposed", "phase", "mfma"], default="transposed",
+                    help="stride-2 ConvTranspose2d: MIOpen's transposed convolution, one 3x3 "
+                         "convolution + pixel shuffle (nets.PHASE_DECONV), or the library's MFMA "
+                         "kernel for bf16 channels-last (nets.MFMA_DECONV)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd, bwd, all-reduce, clip, Adam) in a "
                          "hipGraph and time its replays")
@@ -107,6 +108,7 @@ def main():
     nets.NATIVE_BN = args.bn == "native"
     nets.BIAS_GEMV = args.bias_grad == "gemv"
     nets.PHASE_DECONV = args.deconv == "phase"
+    nets.MFMA_DECONV = args.deconv == "mfma"
 
     torch.manual_seed(0)
     model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,

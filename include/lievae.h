@@ -198,6 +198,17 @@ int lv_fused_exp_action_fwd_repeat(const float* mu, const float* v, const float*
                                    float* ang_out, int64_t n, int L, int C, int transpose,
                                    int repeats, void* stream);
 
+/* ---- decoder ConvTranspose2d(Cin, Cout, 4, stride 2, padding 1) on MFMA (§8 f1) -----
+ * Replaces the MIOpen transposed convolution behind nn.ConvTranspose2d.forward for the
+ * DeconvNet upsampling layers (reference experiments/nets.py:60-75), bf16 NHWC in/out,
+ * fp32 accumulate.  Cin % 8 == 0, Cout % 8 == 0, Cout <= 208.  The weight (Cin, Cout, 4, 4)
+ * bf16 is first repacked into lv_deconv4s2_packed_weight_elems(Cin) bf16 elements (four
+ * output phases x 208 channels x 4*Cin taps); bias (Cout) fp32 or NULL. */
+size_t lv_deconv4s2_packed_weight_elems(int Cin);
+int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, void* stream);
+int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,
+                          int H, int W, int Cin, int Cout, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

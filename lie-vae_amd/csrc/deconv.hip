@@ -1,0 +1,239 @@
+// Decoder transposed convolution on MFMA: ConvTranspose2d(Cin, Cout,
+// kernel 4, stride 2, padding 1) forward, bf16 NHWC, fp32 accumulate -- the three
+// hidden 200 -> 200 upsampling layers of DeconvNet (reference nets.py:60-75; config 3/4
+// decoder).  MIOpen runs these as backward-data convolutions at ~12% of the bf16 MFMA
+// peak (profiles/r03_train_config3_bf16_steady_kernels.txt); here each layer is four
+// implicit GEMMs, one per output phase.
+//
+// Sub-pixel decomposition.  Output pixel (2a + r, 2b + s) only sees input pixels
+// (a + di, b + dj) with di in {r - 1, r}, dj in {s - 1, s}, through kernel tap
+// (ku, kv) = (1 - 2 di + r, 1 - 2 dj + s).  So phase p = 2r + s is a GEMM
+//   Y_p[m, o] = sum_k A_p[m, k] Wt_p[o, k],   m = (n, a, b),  k = t * Cin + c,
+// t = 2 (di - r + 1) + (dj - s + 1) the 2x2 tap, A_p[m, t*Cin + c] = x[n, a+di, b+dj, c]
+// (zero outside the image): M = N·H·W, K = 4·Cin, N = Cout, with no zero taps.  The
+// weight is repacked once per call into Wt[p][o][k] (o padded to kBN with zeros), so a
+// lane's 8 consecutive k of one output channel are one 16-byte load.
+//
+// Tiling (gfx950, v_mfma_f32_16x16x32_bf16): a block of 4 waves computes a 128-pixel x
+// kBN-channel tile of one phase; wave w owns pixel rows [32w, 32w + 32) x all channels
+// (2 x 13 accumulator tiles of 16x16, 104 fp32 registers).  K steps of 32: the next
+// step's A (128 x 32) and B (kBN x 32) pieces are loaded to registers while the current
+// step's MFMAs run, then written to the other LDS buffer (row pitch 80 B: the 16-byte
+// fragment reads of 8 consecutive rows fall in distinct banks).  Epilogue: + bias, round
+// to bf16, stage the tile in LDS, 16-byte stores of whole 2·Cout-byte output rows.
+#include "lv_common.h"
+
+namespace lv {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 128;               // pixels per block tile
+constexpr int kBN = 208;               // output channels per tile (13 x 16; Cout <= kBN)
+constexpr int kNT = kBN / 16;          // 16-wide channel tiles
+constexpr int kBK = 32;                // K per step (one MFMA)
+constexpr int kPitch = kBK + 8;        // LDS row pitch in bf16 (80 B)
+constexpr int kThreads = 256;
+constexpr int kAPieces = kBM * kBK / 8;   // 16-byte pieces per A step (512)
+constexpr int kBPieces = kBN * kBK / 8;   // ... per B step (832)
+constexpr int kAPer = kAPieces / kThreads;                   // 2
+constexpr int kBPer = (kBPieces + kThreads - 1) / kThreads;  // 4
+constexpr size_t kLdsBytes = 2 * (size_t)(kBM + kBN) * kPitch * 2;  // 53,760 B
+
+// Wt[p][o][t*Cin + c] = w[c][o][ku][kv] for o < Cout, 0 for Cout <= o < kBN.
+__global__ void deconv_pack_kernel(const __hip_bfloat16* w, __hip_bfloat16* wt, int Cin, int Cout) {
+  const int64_t K = 4 * (int64_t)Cin;
+  const int64_t total = 4 * (int64_t)kBN * K;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i % K;
+    const int o = (int)((i / K) % kBN);
+    const int p = (int)(i / (K * kBN));
+    const int t = (int)(k / Cin), c = (int)(k % Cin);
+    const int r = p >> 1, s = p & 1;
+    const int di = r - 1 + (t >> 1), dj = s - 1 + (t & 1);
+    const int ku = 1 - 2 * di + r, kv = 1 - 2 * dj + s;
+    wt[i] = o < Cout ? w[(((int64_t)c * Cout + o) * 4 + ku) * 4 + kv] : __float2bfloat16(0.f);
+  }
+}
+
+struct DeconvArgs {
+  const __hip_bfloat16* x;   // (N, H, W, Cin) bf16, channels-last
+  const __hip_bfloat16* wt;  // (4, kBN, 4*Cin) bf16, deconv_pack_kernel
+  const float* bias;         // (Cout) or null
+  __hip_bfloat16* y;         // (N, 2H, 2W, Cout) bf16, channels-last
+  int64_t M;                 // N*H*W pixels per phase
+  int H, W, Cin, Cout;
+};
+
+__global__ __launch_bounds__(kThreads) void deconv_mfma_kernel(DeconvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+  __hip_bfloat16* As = smem;                       // [2][kBM][kPitch]
+  __hip_bfloat16* Bs = smem + 2 * kBM * kPitch;    // [2][kBN][kPitch]
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = blockIdx.y, r = p >> 1, s = p & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * kBM;
+  const int K = 4 * a.Cin;
+  const int nk = K / kBK;
+  const __hip_bfloat16* wtp = a.wt + (int64_t)p * kBN * K;
+
+  // A pieces of this thread: pixel row and the 8-channel group inside the K step
+  int64_t abase[kAPer];  // element offset of (pixel, tap 0 origin) or -1 outside M
+  int arow[kAPer], aq[kAPer], aa[kAPer], ab[kAPer];
+#pragma unroll
+  for (int i = 0; i < kAPer; ++i) {
+    const int pid = tid + kThreads * i;
+    arow[i] = pid >> 2;
+    aq[i] = pid & 3;
+    const int64_t m = m0 + arow[i];
+    if (m < a.M) {
+      const int b = (int)(m % a.W);
+      const int64_t na = m / a.W;
+      aa[i] = (int)(na % a.H);
+      ab[i] = b;
+      abase[i] = (na / a.H) * a.H;  // n * H
+    } else {
+      abase[i] = -1;
+      aa[i] = ab[i] = 0;
+    }
+  }
+  auto load_a = [&](int ks, u32x4 (&ra)[kAPer]) {
+#pragma unroll
+    for (int i = 0; i < kAPer; ++i) {
+      const int k0 = ks * kBK + aq[i] * 8;
+      const int t = k0 / a.Cin, c = k0 - t * a.Cin;
+      const int ia = aa[i] + r - 1 + (t >> 1), ib = ab[i] + s - 1 + (t & 1);
+      ra[i] = u32x4{0u, 0u, 0u, 0u};
+      if (abase[i] >= 0 && ia >= 0 && ia < a.H && ib >= 0 && ib < a.W)
+        ra[i] = *reinterpret_cast<const u32x4*>(a.x + ((abase[i] + ia) * a.W + ib) * a.Cin + c);
+    }
+  };
+  auto load_b = [&](int ks, u32x4 (&rb)[kBPer]) {
+#pragma unroll
+    for (int i = 0; i < kBPer; ++i) {
+      const int pid = tid + kThreads * i;
+      if (pid < kBPieces) {
+        const int o = pid >> 2, q = pid & 3;
+        rb[i] = *reinterpret_cast<const u32x4*>(wtp + (int64_t)o * K + ks * kBK + q * 8);
+      }
+    }
+  };
+  auto store_ab = [&](int buf, const u32x4 (&ra)[kAPer], const u32x4 (&rb)[kBPer]) {
+#pragma unroll
+    for (int i = 0; i < kAPer; ++i)
+      *reinterpret_cast<u32x4*>(As + (buf * kBM + arow[i]) * kPitch + aq[i] * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < kBPer; ++i) {
+      const int pid = tid + kThreads * i;
+      if (pid < kBPieces)
+        *reinterpret_cast<u32x4*>(Bs + (buf * kBN + (pid >> 2)) * kPitch + (pid & 3) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[2][kNT];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[kAPer], rb[kBPer];
+  load_a(0, ra);
+  load_b(0, rb);
+  store_ab(0, ra, rb);
+  __syncthreads();
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) {  // next step's pieces in flight during this step's MFMAs
+      load_a(ks + 1, ra);
+      load_b(ks + 1, rb);
+    }
+    const __hip_bfloat16* Ab = As + (buf * kBM + wave * 32) * kPitch;
+    const __hip_bfloat16* Bb = Bs + buf * kBN * kPitch;
+    bf16x8 af[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      af[mt] = *reinterpret_cast<const bf16x8*>(Ab + (mt * 16 + fr) * kPitch + fk);
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt) {
+      const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bb + (nt * 16 + fr) * kPitch + fk);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bf, acc[mt][nt], 0, 0, 0);
+    }
+    if (ks + 1 < nk) {
+      store_ab(buf ^ 1, ra, rb);  // the other buffer: last read one step ago
+      __syncthreads();
+    }
+  }
+  // epilogue: + bias, bf16, stage [kBM][kBN] in LDS (reuses the A/B buffers)
+  __syncthreads();
+  __hip_bfloat16* Cs = smem;
+  const int cq = (lane >> 4) * 4;
+#pragma unroll
+  for (int nt = 0; nt < kNT; ++nt) {
+    const int o = nt * 16 + fr;
+    const float bo = (a.bias && o < a.Cout) ? a.bias[o] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        Cs[(wave * 32 + mt * 16 + cq + j) * kBN + o] = __float2bfloat16(acc[mt][nt][j] + bo);
+  }
+  __syncthreads();
+  // whole output rows: Cout bf16 per pixel, 16-byte pieces (Cout % 8 == 0)
+  const int pieces = a.Cout / 8;
+  const int H2 = 2 * a.H, W2 = 2 * a.W;
+  for (int e = tid; e < kBM * pieces; e += kThreads) {
+    const int row = e / pieces, q = e - row * pieces;
+    const int64_t m = m0 + row;
+    if (m >= a.M) continue;
+    const int b = (int)(m % a.W);
+    const int64_t na = m / a.W;
+    const int aa_ = (int)(na % a.H);
+    const int64_t n = na / a.H;
+    __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 8;
+    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + row * kBN + q * 8);
+  }
+}
+
+}  // namespace
+}  // namespace lv
+
+using namespace lv;
+
+extern "C" {
+
+size_t lv_deconv4s2_packed_weight_elems(int Cin) { return 4 * (size_t)kBN * 4 * (size_t)Cin; }
+
+int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(w && wt, "null pointer");
+  LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
+  LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 8 == 0, "Cout must be a multiple of 8 in [8, %d] (got %d)", kBN, Cout);
+  hipLaunchKernelGGL(deconv_pack_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream,
+                     (const __hip_bfloat16*)w, (__hip_bfloat16*)wt, Cin, Cout);
+  LV_RETURN_LAUNCH("deconv_pack_kernel");
+}
+
+int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,
+                          int H, int W, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
+  LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
+  LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 8 == 0, "Cout must be a multiple of 8 in [8, %d] (got %d)", kBN, Cout);
+  if (N == 0) return LV_OK;
+  LV_CHECK_ARG(x && wt && y, "null pointer");
+  const int64_t M = N * H * W;
+  LV_CHECK_ARG((M + kBM - 1) / kBM <= 0x7fffffff, "batch too large");
+  DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout};
+  hipLaunchKernelGGL(deconv_mfma_kernel, dim3((unsigned)((M + kBM - 1) / kBM), 4), dim3(kThreads), kLdsBytes,
+                     (hipStream_t)stream, a);
+  LV_RETURN_LAUNCH("deconv_mfma_kernel");
+}
+
+}  // extern "C"

@@ -135,6 +135,65 @@ class BiasGemvConvTranspose2d(nn.ConvTranspose2d):
 
 
 PHASE_DECONV = False  # off: 10.5 vs 7.4 ms (bf16), 22.1 vs 15.2 ms (f32)
+# The stride-2 ConvTranspose2d forward on the library's MFMA kernel (lv_deconv4s2_fwd_bf16,
+# csrc/deconv.hip) when it runs in bf16 (autocast) on channels-last inputs; fp32 / NCHW /
+# unsupported shapes keep MIOpen.  The backward stays on PyTorch's convolution_backward.
+MFMA_DECONV = False
+
+
+class _Deconv4s2(torch.autograd.Function):
+    """y = conv_transpose2d(x, w, b, stride 2, padding 1), k = 4: forward on the MFMA
+    kernel (x, w bf16; b fp32 added before the bf16 rounding), backward through
+    aten.convolution_backward on the saved bf16 operands (what MIOpen computes for the
+    plain layer)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        from .. import _lib
+        N, Cin, H, W = x.shape
+        Cout = w.shape[1]
+        wc = w.contiguous()
+        wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems(Cin), device=x.device,
+                         dtype=torch.bfloat16)
+        y = torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=torch.bfloat16,
+                        memory_format=torch.channels_last)
+        st = _lib.stream()
+        _lib.call("lv_deconv4s2_pack_weight_bf16", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
+        _lib.call("lv_deconv4s2_fwd_bf16", x.data_ptr(), wt.data_ptr(),
+                  None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, st)
+        ctx.save_for_backward(x, wc)
+        ctx.has_bias = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx, gw, gb = torch.ops.aten.convolution_backward(
+            gy.to(torch.bfloat16), x, w, [w.shape[1]] if ctx.has_bias else None, [2, 2], [1, 1],
+            [1, 1], True, [0, 0], 1, [True, True, ctx.has_bias])
+        return gx, gw, (gb.float() if ctx.has_bias else None)
+
+
+class MfmaConvTranspose2d(nn.ConvTranspose2d):
+    """nn.ConvTranspose2d (same parameters / state_dict) whose k4 s2 p1 forward runs on
+    the MFMA kernel for bf16 channels-last inputs (autocast bf16, or bf16 tensors)."""
+
+    def _mfma_ok(self, x):
+        return (x.is_cuda and x.dim() == 4 and _cl(x) and self.kernel_size == (4, 4)
+                and self.stride == (2, 2) and self.padding == (1, 1)
+                and self.output_padding == (0, 0) and self.dilation == (1, 1)
+                and self.groups == 1 and self.in_channels % 8 == 0
+                and self.out_channels % 8 == 0 and self.out_channels <= 208)
+
+    def forward(self, x, output_size=None):
+        bf16 = x.dtype == torch.bfloat16 or (
+            torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        if output_size is not None or not bf16 or not self._mfma_ok(x):
+            return super().forward(x, output_size)
+        with torch.autocast("cuda", enabled=False):
+            xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            return _Deconv4s2.apply(xb, self.weight.to(torch.bfloat16),
+                                    None if self.bias is None else self.bias.float())
 
 
 class PhaseConvTranspose2d(nn.ConvTranspose2d):
@@ -187,6 +246,8 @@ def _convt(*a):
 
 
 def _convt_s2(*a):
+    if MFMA_DECONV:
+        return MfmaConvTranspose2d(*a)
     if PHASE_DECONV:
         return PhaseConvTranspose2d(*a)
     return (BiasGemvConvTranspose2d if BIAS_GEMV else nn.ConvTranspose2d)(*a)

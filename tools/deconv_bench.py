@@ -1,0 +1,38 @@
+"""Decoder ConvTranspose2d(200, 200, 4, 2, 1) forward at the config-3 batch (512), bf16
+NHWC: MIOpen (torch conv_transpose2d) vs the library's MFMA kernel (lv_deconv4s2_fwd_bf16,
+pack + GEMM), HIP events over 50 calls each.  FLOPs = 2 * N * Cin * Cout * 16 * H * W."""
+import json
+import sys
+import torch
+sys.path[:0] = ["lie-vae_amd", "."]
+from lie_vae.experiments.nets import _Deconv4s2
+
+dev = torch.device("cuda:0")
+torch.backends.cudnn.benchmark = True
+res = []
+for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16)]:
+    x = torch.randn(N, C, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(C, C, 4, 4, device=dev) * 0.05).to(torch.bfloat16)
+    b = torch.randn(C, device=dev)
+    wcl = w.contiguous(memory_format=torch.channels_last)
+    flops = 2.0 * N * C * C * 16 * H * H
+    row = {"N": N, "Cin": C, "Cout": C, "H_in": H, "GFLOP": flops / 1e9}
+    for tag, fn in (("miopen", lambda: torch.nn.functional.conv_transpose2d(x, wcl, b.to(torch.bfloat16), 2, 1)),
+                    ("mfma", lambda: _Deconv4s2.apply(x, w, b))):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / 50
+        row[tag + "_us"] = us
+        row[tag + "_TFLOPs"] = flops / us / 1e6
+    ref = torch.nn.functional.conv_transpose2d(x.float(), w.float(), b, 2, 1)
+    y = _Deconv4s2.apply(x, w, b).float()
+    row["max_rel_err_vs_f32"] = float(((y - ref).abs().max() / ref.abs().max()).item())
+    res.append(row)
+    print(json.dumps(row), flush=True)
