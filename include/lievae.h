@@ -208,6 +208,9 @@ size_t lv_deconv4s2_packed_weight_elems(int Cin);
 int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, void* stream);
 int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                           int H, int W, int Cin, int Cout, void* stream);
+/* Same with an explicit pixel-tile height (0 = the default, 128 or 256; A/B). */
+int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y,
+                               int64_t N, int H, int W, int Cin, int Cout, int bm, void* stream);
 
 #ifdef __cplusplus
 }

@@ -30,17 +30,21 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 128;               // pixels per block tile
 constexpr int kBN = 208;               // output channels per tile (13 x 16; Cout <= kBN)
 constexpr int kNT = kBN / 16;          // 16-wide channel tiles
 constexpr int kBK = 32;                // K per step (one MFMA)
 constexpr int kPitch = kBK + 8;        // LDS row pitch in bf16 (80 B)
-constexpr int kThreads = 256;
-constexpr int kAPieces = kBM * kBK / 8;   // 16-byte pieces per A step (512)
-constexpr int kBPieces = kBN * kBK / 8;   // ... per B step (832)
-constexpr int kAPer = kAPieces / kThreads;                   // 2
-constexpr int kBPer = (kBPieces + kThreads - 1) / kThreads;  // 4
-constexpr size_t kLdsBytes = 2 * (size_t)(kBM + kBN) * kPitch * 2;  // 53,760 B
+constexpr int kBPieces = kBN * kBK / 8;   // 16-byte pieces per B step (832)
+// BM pixels per block tile, BM / 32 waves (each 32 pixel rows x kBN channels)
+template <int BM>
+struct DeconvTile {
+  static constexpr int kThreads = BM * 2;
+  static constexpr int kAPer = BM * kBK / 8 / kThreads;                 // 2
+  static constexpr int kBPer = (kBPieces + kThreads - 1) / kThreads;    // 4 / 2
+  static constexpr int kStageRows = BM <= 128 ? BM : 128;               // epilogue pass rows
+  static constexpr size_t kLds = 2 * (size_t)(BM + kBN) * kPitch * 2;   // 53,760 / 74,240 B
+  static_assert((size_t)kStageRows * kBN * 2 <= kLds, "epilogue stage fits the A/B buffers");
+};
 
 // Wt[p][o][t*Cin + c] = w[c][o][ku][kv] for o < Cout, 0 for Cout <= o < kBN.
 __global__ void deconv_pack_kernel(const __hip_bfloat16* w, __hip_bfloat16* wt, int Cin, int Cout) {
@@ -68,7 +72,11 @@ struct DeconvArgs {
   int H, W, Cin, Cout;
 };
 
-__global__ __launch_bounds__(kThreads) void deconv_mfma_kernel(DeconvArgs a) {
+template <int BM>
+__global__ __launch_bounds__(BM * 2) void deconv_mfma_kernel(DeconvArgs a) {
+  using T = DeconvTile<BM>;
+  constexpr int kThreads = T::kThreads, kAPer = T::kAPer, kBPer = T::kBPer;
+  constexpr int kBM = BM;
   extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
   __hip_bfloat16* As = smem;                       // [2][kBM][kPitch]
   __hip_bfloat16* Bs = smem + 2 * kBM * kPitch;    // [2][kBN][kPitch]
@@ -170,34 +178,41 @@ __global__ __launch_bounds__(kThreads) void deconv_mfma_kernel(DeconvArgs a) {
       __syncthreads();
     }
   }
-  // epilogue: + bias, bf16, stage [kBM][kBN] in LDS (reuses the A/B buffers)
-  __syncthreads();
+  // epilogue: + bias, bf16, stage [rows][kBN] in LDS (reuses the A/B buffers) in passes
+  // of kStageRows pixel rows, then 16-byte stores of whole output rows (Cout % 8 == 0)
   __hip_bfloat16* Cs = smem;
   const int cq = (lane >> 4) * 4;
-#pragma unroll
-  for (int nt = 0; nt < kNT; ++nt) {
-    const int o = nt * 16 + fr;
-    const float bo = (a.bias && o < a.Cout) ? a.bias[o] : 0.f;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        Cs[(wave * 32 + mt * 16 + cq + j) * kBN + o] = __float2bfloat16(acc[mt][nt][j] + bo);
-  }
-  __syncthreads();
-  // whole output rows: Cout bf16 per pixel, 16-byte pieces (Cout % 8 == 0)
   const int pieces = a.Cout / 8;
   const int H2 = 2 * a.H, W2 = 2 * a.W;
-  for (int e = tid; e < kBM * pieces; e += kThreads) {
-    const int row = e / pieces, q = e - row * pieces;
-    const int64_t m = m0 + row;
-    if (m >= a.M) continue;
-    const int b = (int)(m % a.W);
-    const int64_t na = m / a.W;
-    const int aa_ = (int)(na % a.H);
-    const int64_t n = na / a.H;
-    __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 8;
-    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + row * kBN + q * 8);
+  constexpr int SR = T::kStageRows;
+#pragma unroll
+  for (int pass = 0; pass < kBM / SR; ++pass) {
+    __syncthreads();
+    if (wave * 32 / SR == pass) {
+#pragma unroll
+      for (int nt = 0; nt < kNT; ++nt) {
+        const int o = nt * 16 + fr;
+        const float bo = (a.bias && o < a.Cout) ? a.bias[o] : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            Cs[(wave * 32 - pass * SR + mt * 16 + cq + j) * kBN + o] =
+                __float2bfloat16(acc[mt][nt][j] + bo);
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < SR * pieces; e += kThreads) {
+      const int row = e / pieces, q = e - row * pieces;
+      const int64_t m = m0 + pass * SR + row;
+      if (m >= a.M) continue;
+      const int b = (int)(m % a.W);
+      const int64_t na = m / a.W;
+      const int aa_ = (int)(na % a.H);
+      const int64_t n = na / a.H;
+      __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 8;
+      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + row * kBN + q * 8);
+    }
   }
 }
 
@@ -206,7 +221,20 @@ __global__ __launch_bounds__(kThreads) void deconv_mfma_kernel(DeconvArgs a) {
 
 using namespace lv;
 
+constexpr int kDeconvAutoBM = 128;
+
+namespace {
+template <int BM>
+int launch_deconv(const DeconvArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(deconv_mfma_kernel<BM>, dim3((unsigned)((a.M + BM - 1) / BM), 4),
+                     dim3(DeconvTile<BM>::kThreads), DeconvTile<BM>::kLds, st, a);
+  LV_RETURN_LAUNCH("deconv_mfma_kernel");
+}
+}  // namespace
+
 extern "C" {
+int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
+                               int H, int W, int Cin, int Cout, int bm, void* stream);
 
 size_t lv_deconv4s2_packed_weight_elems(int Cin) { return 4 * (size_t)kBN * 4 * (size_t)Cin; }
 
@@ -222,6 +250,11 @@ int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, vo
 
 int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                           int H, int W, int Cin, int Cout, void* stream) {
+  return lv_deconv4s2_fwd_bf16_tile(x, wt, bias, y, N, H, W, Cin, Cout, 0, stream);
+}
+
+int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
+                               int H, int W, int Cin, int Cout, int bm, void* stream) {
   clear_error();
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
@@ -229,11 +262,11 @@ int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void
   if (N == 0) return LV_OK;
   LV_CHECK_ARG(x && wt && y, "null pointer");
   const int64_t M = N * H * W;
-  LV_CHECK_ARG((M + kBM - 1) / kBM <= 0x7fffffff, "batch too large");
+  LV_CHECK_ARG((M + 127) / 128 <= 0x7fffffff, "batch too large");
+  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256, "tile rows must be 0 (auto), 128 or 256");
   DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout};
-  hipLaunchKernelGGL(deconv_mfma_kernel, dim3((unsigned)((M + kBM - 1) / kBM), 4), dim3(kThreads), kLdsBytes,
-                     (hipStream_t)stream, a);
-  LV_RETURN_LAUNCH("deconv_mfma_kernel");
+  if (bm == 0) bm = kDeconvAutoBM;
+  return bm == 256 ? launch_deconv<256>(a, (hipStream_t)stream) : launch_deconv<128>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -17,8 +17,17 @@ for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16)]:
     wcl = w.contiguous(memory_format=torch.channels_last)
     flops = 2.0 * N * C * C * 16 * H * H
     row = {"N": N, "Cin": C, "Cout": C, "H_in": H, "GFLOP": flops / 1e9}
+    from lie_vae import _lib
+    wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems(C), device=dev, dtype=torch.bfloat16)
+    _lib.call("lv_deconv4s2_pack_weight_bf16", w.data_ptr(), wt.data_ptr(), C, C, _lib.stream())
+    yk = torch.empty(N, C, 2 * H, 2 * H, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
+
+    def kern(bm):
+        _lib.call("lv_deconv4s2_fwd_bf16_tile", x.data_ptr(), wt.data_ptr(), b.data_ptr(), yk.data_ptr(),
+                  N, H, H, C, C, bm, _lib.stream())
     for tag, fn in (("miopen", lambda: torch.nn.functional.conv_transpose2d(x, wcl, b.to(torch.bfloat16), 2, 1)),
-                    ("mfma", lambda: _Deconv4s2.apply(x, w, b))):
+                    ("mfma", lambda: _Deconv4s2.apply(x, w, b)),
+                    ("gemm_bm128", lambda: kern(128)), ("gemm_bm256", lambda: kern(256))):
         for _ in range(5):
             fn()
         torch.cuda.synchronize()
