@@ -14,10 +14,11 @@
 // weight is repacked once per call into Wt[p][o][k] (o padded to kBN with zeros), so a
 // lane's 8 consecutive k of one output channel are one 16-byte load.
 //
-// Tiling (gfx950, v_mfma_f32_16x16x32_bf16): a block of 4 waves computes a 128-pixel x
-// kBN-channel tile of one phase; wave w owns pixel rows [32w, 32w + 32) x all channels
-// (2 x 13 accumulator tiles of 16x16, 104 fp32 registers).  K steps of 32: the next
-// step's A (128 x 32) and B (kBN x 32) pieces are loaded to registers while the current
+// Tiling (gfx950, v_mfma_f32_16x16x32_bf16): a block of BM / 32 waves (BM = 256 by
+// default: the weight tile is read from L2 once per 256 pixels; 128 ran 1.1-1.8x slower)
+// computes a BM-pixel x kBN-channel tile of one phase; wave w owns pixel rows [32w, 32w+32)
+// x all channels (2 x 13 accumulator tiles of 16x16, 104 fp32 registers).  K steps of 32:
+// the next step's A (BM x 32) and B (kBN x 32) pieces are loaded to registers while the current
 // step's MFMAs run, then written to the other LDS buffer (row pitch 80 B: the 16-byte
 // fragment reads of 8 consecutive rows fall in distinct banks).  Epilogue: + bias, round
 // to bf16, stage the tile in LDS, 16-byte stores of whole 2·Cout-byte output rows.
@@ -46,20 +47,23 @@ struct DeconvTile {
   static_assert((size_t)kStageRows * kBN * 2 <= kLds, "epilogue stage fits the A/B buffers");
 };
 
-// Wt[p][o][t*Cin + c] = w[c][o][ku][kv] for o < Cout, 0 for Cout <= o < kBN.
+// Wt[p][o][t*Cin + c] = w[c][o][ku][kv] for o < Cout, 0 for Cout <= o < kBN.  One thread
+// per 8 consecutive k of one (phase, channel): 8 gathered 2-byte reads of the (L2-resident)
+// weight, one 16-byte store.
 __global__ void deconv_pack_kernel(const __hip_bfloat16* w, __hip_bfloat16* wt, int Cin, int Cout) {
-  const int64_t K = 4 * (int64_t)Cin;
-  const int64_t total = 4 * (int64_t)kBN * K;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = i % K;
-    const int o = (int)((i / K) % kBN);
-    const int p = (int)(i / (K * kBN));
-    const int t = (int)(k / Cin), c = (int)(k % Cin);
+  const int K = 4 * Cin, kg = K / 8;
+  const int total = 4 * kBN * kg;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i % kg, o = (i / kg) % kBN, p = i / (kg * kBN);
+    const int k0 = 8 * g, t = k0 / Cin, c0 = k0 - t * Cin;
     const int r = p >> 1, s = p & 1;
     const int di = r - 1 + (t >> 1), dj = s - 1 + (t & 1);
-    const int ku = 1 - 2 * di + r, kv = 1 - 2 * dj + s;
-    wt[i] = o < Cout ? w[(((int64_t)c * Cout + o) * 4 + ku) * 4 + kv] : __float2bfloat16(0.f);
+    const int tap = (1 - 2 * di + r) * 4 + (1 - 2 * dj + s);
+    __hip_bfloat16 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = o < Cout ? w[((c0 + e) * Cout + o) * 16 + tap] : __float2bfloat16(0.f);
+    *reinterpret_cast<u32x4*>(wt + ((int64_t)(p * kBN + o) * K + k0)) = *reinterpret_cast<const u32x4*>(v);
   }
 }
 
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(BM * 2) void deconv_mfma_kernel(DeconvArgs a) {
 
 using namespace lv;
 
-constexpr int kDeconvAutoBM = 128;
+constexpr int kDeconvAutoBM = 256;  // 1.6-2.1x MIOpen at batch 512 (profiles/r03_deconv_mfma.txt)
 
 namespace {
 template <int BM>
@@ -243,7 +247,8 @@ int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, vo
   LV_CHECK_ARG(w && wt, "null pointer");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
   LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 8 == 0, "Cout must be a multiple of 8 in [8, %d] (got %d)", kBN, Cout);
-  hipLaunchKernelGGL(deconv_pack_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream,
+  LV_CHECK_ARG((int64_t)Cin * Cout * 16 < (1ll << 31), "weight too large");
+  hipLaunchKernelGGL(deconv_pack_kernel, dim3(ceil_div(4 * kBN * (Cin / 2), 256)), dim3(256), 0, (hipStream_t)stream,
                      (const __hip_bfloat16*)w, (__hip_bfloat16*)wt, Cin, Cout);
   LV_RETURN_LAUNCH("deconv_pack_kernel");
 }
