@@ -208,6 +208,13 @@ size_t lv_deconv4s2_packed_weight_elems(int Cin);
 int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, void* stream);
 int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                           int H, int W, int Cin, int Cout, void* stream);
+/* The same layer with Cout <= 4 (the decoder's RGB output layer, nets.py:74): one GEMM row
+ * per output quad over the 3x3 input neighbourhood, all four phases x Cout in one 16-wide
+ * MFMA tile.  Weight repacked into lv_deconv4s2_small_packed_weight_elems(Cin) bf16. */
+size_t lv_deconv4s2_small_packed_weight_elems(int Cin);
+int lv_deconv4s2_small_pack_weight_bf16(const void* w, void* wq, int Cin, int Cout, void* stream);
+int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias, void* y,
+                                int64_t N, int H, int W, int Cin, int Cout, void* stream);
 /* Same with an explicit pixel-tile height (0 = the default, 128 or 256; A/B). */
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y,
                                int64_t N, int H, int W, int Cin, int Cout, int bm, void* stream);

@@ -220,6 +220,156 @@ __global__ __launch_bounds__(BM * 2) void deconv_mfma_kernel(DeconvArgs a) {
   }
 }
 
+
+// ----------------------------------------------------- small-Cout decoder layer
+// The decoder's last layer ConvTranspose2d(200, 3, 4, 2, 1) (nets.py:74): an N = 3
+// GEMM per phase wastes an MFMA tile and MIOpen runs it at ~10 TFLOP/s (1 ms per forward
+// at batch 512, profiles/r03_conv_layers.txt).  Here one GEMM row is an output QUAD
+// (2a + r, 2b + s), r, s in {0, 1}: its four pixels see only the 3x3 input neighbourhood
+// of (a, b), so
+//   Y[quad, (p, o)] = sum_{nbr, c} X[a + na - 1, b + nb - 1, c] Wq[nbr, c, (p, o)],
+// with Wq[nbr, c, (p, o)] = w[c, o, ku, kv] when nbr = (na, nb) is a tap of phase p (else
+// 0): K = 9 x Cin, N = 4·Cout <= 16 -- one 16x16x32 MFMA column tile for all phases.
+// A block covers 8 x 16 quads of one image; per 32-channel chunk the 10 x 18 input pixels
+// of that region are staged once in LDS and the nine neighbour offsets are nine K steps
+// read from it (no im2col), so each input byte crosses HBM once (+ a halo).  Channels
+// beyond Cin read as zero (K padded to a multiple of 32 per neighbour).
+constexpr int kSqH = 8, kSqW = 16;                      // quads per block
+constexpr int kSiH = kSqH + 2, kSiW = kSqW + 2;         // staged input pixels
+constexpr int kSPitch = 40;                              // bf16 per staged pixel (32 + pad)
+constexpr int kSmallThreads = 256;
+constexpr int kSmallMaxCout = 4;
+
+// Wq[chunk][nbr][n][32] (n = p * Cout + o padded to 16), zeros where nbr is not a tap of p
+__global__ void deconv_small_pack_kernel(const __hip_bfloat16* w, __hip_bfloat16* wq, int Cin, int Cout) {
+  const int nch = (Cin + 31) / 32;
+  const int total = nch * 9 * 16 * 32;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cl = i % 32, n = (i / 32) % 16, nbr = (i / 512) % 9, ch = i / (512 * 9);
+    const int c = ch * 32 + cl;
+    const int p = n / Cout, o = n - p * Cout;
+    float v = 0.f;
+    if (c < Cin && p < 4) {
+      const int r = p >> 1, s = p & 1;
+      const int di = nbr / 3 - 1, dj = nbr % 3 - 1;           // input offset of the neighbour
+      if ((di == r - 1 || di == r) && (dj == s - 1 || dj == s)) {
+        const int ku = 1 - 2 * di + r, kv = 1 - 2 * dj + s;
+        v = __bfloat162float(w[((c * Cout + o) * 4 + ku) * 4 + kv]);
+      }
+    }
+    wq[i] = __float2bfloat16(v);
+  }
+}
+
+struct DeconvSmallArgs {
+  const __hip_bfloat16* x;    // (N, H, W, Cin) bf16 channels-last
+  const __hip_bfloat16* wq;   // deconv_small_pack_kernel
+  const float* bias;          // (Cout) or null
+  __hip_bfloat16* y;          // (N, 2H, 2W, Cout) bf16 channels-last
+  int H, W, Cin, Cout, tiles_w;
+};
+
+__global__ __launch_bounds__(kSmallThreads) void deconv_small_kernel(DeconvSmallArgs a) {
+  __shared__ __attribute__((aligned(16))) __hip_bfloat16 xs[2][kSiH * kSiW * kSPitch];  // 2 x 14.4 KB
+  __shared__ __attribute__((aligned(16))) __hip_bfloat16 ws[2][9 * 16 * kSPitch];         // 2 x 11.5 KB
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_img = blockIdx.y;
+  const int ta = blockIdx.x / a.tiles_w, tb = blockIdx.x - ta * a.tiles_w;
+  const int a0 = ta * kSqH, b0 = tb * kSqW;
+  const int nch = (a.Cin + 31) / 32;
+  const __hip_bfloat16* ximg = a.x + (int64_t)n_img * a.H * a.W * a.Cin;
+  constexpr int kXPieces = kSiH * kSiW * 4;   // 16-byte pieces of an input chunk (720)
+  constexpr int kWPieces = 9 * 16 * 4;        // ... of a weight chunk (576)
+  constexpr int kXPer = (kXPieces + kSmallThreads - 1) / kSmallThreads;  // 3
+  constexpr int kWPer = (kWPieces + kSmallThreads - 1) / kSmallThreads;  // 3
+  u32x4 rx[kXPer], rw[kWPer];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < kXPer; ++i) {
+      const int pid = tid + kSmallThreads * i;
+      rx[i] = u32x4{0u, 0u, 0u, 0u};
+      if (pid < kXPieces) {
+        const int px = pid >> 2, q = pid & 3;
+        const int ia = a0 - 1 + px / kSiW, ib = b0 - 1 + px % kSiW;
+        const int c = ch * 32 + q * 8;
+        if (ia >= 0 && ia < a.H && ib >= 0 && ib < a.W && c < a.Cin)
+          rx[i] = *reinterpret_cast<const u32x4*>(ximg + ((int64_t)ia * a.W + ib) * a.Cin + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kWPer; ++i) {
+      const int pid = tid + kSmallThreads * i;
+      if (pid < kWPieces) rw[i] = *reinterpret_cast<const u32x4*>(a.wq + ((int64_t)ch * kWPieces + pid) * 8);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < kXPer; ++i) {
+      const int pid = tid + kSmallThreads * i;
+      if (pid < kXPieces) *reinterpret_cast<u32x4*>(&xs[buf][(pid >> 2) * kSPitch + (pid & 3) * 8]) = rx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kWPer; ++i) {
+      const int pid = tid + kSmallThreads * i;
+      if (pid < kWPieces) *reinterpret_cast<u32x4*>(&ws[buf][(pid >> 2) * kSPitch + (pid & 3) * 8]) = rw[i];
+    }
+  };
+  // wave w: quad rows 2w, 2w + 1 (one 16-quad M tile each); lane row = quad column
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) load(ch + 1);
+#pragma unroll
+    for (int nbr = 0; nbr < 9; ++nbr) {
+      const int na = nbr / 3, nb = nbr % 3;
+      const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&ws[buf][(nbr * 16 + fr) * kSPitch + fk]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int qr = 2 * wave + mt;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(
+            &xs[buf][((qr + na) * kSiW + fr + nb) * kSPitch + fk]);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[mt], 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nch) {
+      store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // epilogue: C column n = fr -> (phase p, channel o); rows -> quad columns (lane>>4)*4 + j.
+  // Stage the block's (2 kSqH) x (2 kSqW) x Cout output pixels in LDS (xs buffer), then
+  // write each output row's 2 kSqW * Cout contiguous values.
+  __syncthreads();
+  __hip_bfloat16* os = &xs[0][0];
+  const int Co = a.Cout, OW = 2 * kSqW;
+  const int p = fr / Co, o = fr - p * Co;
+  if (p < 4) {
+    const float bo = a.bias ? a.bias[o] : 0.f;
+    const int r = p >> 1, s = p & 1;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int qr = 2 * wave + mt, qc = (lane >> 4) * 4 + j;
+        os[((2 * qr + r) * OW + 2 * qc + s) * Co + o] = __float2bfloat16(acc[mt][j] + bo);
+      }
+  }
+  __syncthreads();
+  const int H2 = 2 * a.H, W2 = 2 * a.W;
+  const int ocols = min(OW, W2 - 2 * b0);   // valid output columns of this tile
+  const int orows = min(2 * kSqH, H2 - 2 * a0);
+  const int rowel = ocols * Co;             // contiguous elements per output row
+  for (int e = tid; e < orows * rowel; e += kSmallThreads) {
+    const int rr = e / rowel, k = e - rr * rowel;
+    a.y[(((int64_t)n_img * H2 + 2 * a0 + rr) * W2 + 2 * b0) * Co + k] = os[rr * OW * Co + k];
+  }
+}
+
 }  // namespace
 }  // namespace lv
 
@@ -272,6 +422,35 @@ int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias,
   DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout};
   if (bm == 0) bm = kDeconvAutoBM;
   return bm == 256 ? launch_deconv<256>(a, (hipStream_t)stream) : launch_deconv<128>(a, (hipStream_t)stream);
+}
+
+size_t lv_deconv4s2_small_packed_weight_elems(int Cin) { return (size_t)((Cin + 31) / 32) * 9 * 16 * 32; }
+
+int lv_deconv4s2_small_pack_weight_bf16(const void* w, void* wq, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(w && wq, "null pointer");
+  LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
+  LV_CHECK_ARG(Cout >= 1 && Cout <= kSmallMaxCout, "Cout must be in [1, %d] (got %d)", kSmallMaxCout, Cout);
+  const int total = (int)lv_deconv4s2_small_packed_weight_elems(Cin);
+  hipLaunchKernelGGL(deconv_small_pack_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const __hip_bfloat16*)w, (__hip_bfloat16*)wq, Cin, Cout);
+  LV_RETURN_LAUNCH("deconv_small_pack_kernel");
+}
+
+int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias, void* y, int64_t N,
+                                int H, int W, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
+  LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
+  LV_CHECK_ARG(Cout >= 1 && Cout <= kSmallMaxCout, "Cout must be in [1, %d] (got %d)", kSmallMaxCout, Cout);
+  LV_CHECK_ARG(N <= 65535, "batch must be <= 65535 (grid y)");
+  if (N == 0) return LV_OK;
+  LV_CHECK_ARG(x && wq && y, "null pointer");
+  const int th = (H + kSqH - 1) / kSqH, tw = (W + kSqW - 1) / kSqW;
+  DeconvSmallArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wq, bias, (__hip_bfloat16*)y, H, W, Cin, Cout, tw};
+  hipLaunchKernelGGL(deconv_small_kernel, dim3(th * tw, (unsigned)N), dim3(kSmallThreads), 0,
+                     (hipStream_t)stream, a);
+  LV_RETURN_LAUNCH("deconv_small_kernel");
 }
 
 }  // extern "C"

@@ -67,10 +67,12 @@ for _name in ("lv_so3_exp_fwd", "lv_so3_exp_bwd", "lv_so3_sample_fwd", "lv_so3_s
 _SIGS["lv_deconv4s2_pack_weight_bf16"] = [_P, _P, _I, _I, _P]
 _SIGS["lv_deconv4s2_fwd_bf16"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_fwd_bf16_tile"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
+_SIGS["lv_deconv4s2_small_pack_weight_bf16"] = [_P, _P, _I, _I, _P]
+_SIGS["lv_deconv4s2_small_fwd_bf16"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _P]
 _RESTYPES = {"lv_group_action_bwd_workspace": _SZ, "lv_last_error": ctypes.c_char_p,
-             "lv_deconv4s2_packed_weight_elems": _SZ}
+             "lv_deconv4s2_packed_weight_elems": _SZ, "lv_deconv4s2_small_packed_weight_elems": _SZ}
 _SIGS_EXTRA = {"lv_group_action_bwd_workspace": [_I64, _I, _I, _I], "lv_last_error": [],
-               "lv_deconv4s2_packed_weight_elems": [_I]}
+               "lv_deconv4s2_packed_weight_elems": [_I], "lv_deconv4s2_small_packed_weight_elems": [_I]}
 
 EXPORTED = sorted(list(_SIGS) + list(_SIGS_EXTRA))
 

@@ -153,13 +153,15 @@ class _Deconv4s2(torch.autograd.Function):
         N, Cin, H, W = x.shape
         Cout = w.shape[1]
         wc = w.contiguous()
-        wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems(Cin), device=x.device,
+        small = Cout <= 4  # the RGB output layer: quad GEMM over the 3x3 neighbourhood
+        pre = "lv_deconv4s2_small_" if small else "lv_deconv4s2_"
+        wt = torch.empty(getattr(_lib.load(), pre + "packed_weight_elems")(Cin), device=x.device,
                          dtype=torch.bfloat16)
         y = torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=torch.bfloat16,
                         memory_format=torch.channels_last)
         st = _lib.stream()
-        _lib.call("lv_deconv4s2_pack_weight_bf16", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
-        _lib.call("lv_deconv4s2_fwd_bf16", x.data_ptr(), wt.data_ptr(),
+        _lib.call(pre + "pack_weight_bf16", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
+        _lib.call(pre + "fwd_bf16", x.data_ptr(), wt.data_ptr(),
                   None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, st)
         ctx.save_for_backward(x, wc)
         ctx.has_bias = b is not None
@@ -183,7 +185,8 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
                 and self.stride == (2, 2) and self.padding == (1, 1)
                 and self.output_padding == (0, 0) and self.dilation == (1, 1)
                 and self.groups == 1 and self.in_channels % 8 == 0
-                and self.out_channels % 8 == 0 and self.out_channels <= 208)
+                and ((self.out_channels % 8 == 0 and self.out_channels <= 208)
+                     or self.out_channels <= 4) and x.shape[0] <= 65535)
 
     def forward(self, x, output_size=None):
         bf16 = x.dtype == torch.bfloat16 or (

@@ -515,10 +515,13 @@ def test_config4_dp_two_ranks_share_one_gpu(tmp_path):
 
 # ----------------------------------------------- decoder ConvTranspose2d on MFMA (§8 f1)
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(3, 200, 200, 16, 16), (4, 200, 200, 4, 4),
-                                           (2, 16, 8, 5, 3), (5, 64, 200, 7, 9)])
+                                           (2, 16, 8, 5, 3), (5, 64, 200, 7, 9),
+                                           (3, 200, 3, 32, 32), (2, 40, 1, 9, 21),
+                                           (2, 200, 4, 17, 16)])
 def test_mfma_deconv_matches_conv_transpose(gpu_device, N, Cin, Cout, H, W):
     """lv_deconv4s2_fwd_bf16 (csrc/deconv.hip: four sub-pixel implicit GEMMs on
-    v_mfma_f32_16x16x32_bf16) against conv_transpose2d(stride 2, padding 1) evaluated in
+    v_mfma_f32_16x16x32_bf16) and, for Cout <= 4, lv_deconv4s2_small_fwd_bf16 (one quad GEMM
+    over the 3x3 neighbourhood) against conv_transpose2d(stride 2, padding 1) evaluated in
     float64 on the same bf16 operands: fp32 accumulation, one bf16 rounding of the output
     (|err| <= 2^-8 |ref| + 1e-3 rms(ref)); ragged pixel tiles, border taps, small C."""
     from lie_vae.experiments.nets import _Deconv4s2

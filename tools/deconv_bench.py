@@ -10,24 +10,29 @@ from lie_vae.experiments.nets import _Deconv4s2
 dev = torch.device("cuda:0")
 torch.backends.cudnn.benchmark = True
 res = []
-for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16)]:
-    x = torch.randn(N, C, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(C, C, 4, 4, device=dev) * 0.05).to(torch.bfloat16)
-    b = torch.randn(C, device=dev)
+for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16), (512, 3, 32)]:
+    Ci, Co = 200, C
+    x = torch.randn(N, Ci, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Ci, Co, 4, 4, device=dev) * 0.05).to(torch.bfloat16)
+    b = torch.randn(Co, device=dev)
     wcl = w.contiguous(memory_format=torch.channels_last)
-    flops = 2.0 * N * C * C * 16 * H * H
-    row = {"N": N, "Cin": C, "Cout": C, "H_in": H, "GFLOP": flops / 1e9}
+    flops = 2.0 * N * Ci * Co * 16 * H * H
+    row = {"N": N, "Cin": Ci, "Cout": Co, "H_in": H, "GFLOP": flops / 1e9}
     from lie_vae import _lib
-    wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems(C), device=dev, dtype=torch.bfloat16)
-    _lib.call("lv_deconv4s2_pack_weight_bf16", w.data_ptr(), wt.data_ptr(), C, C, _lib.stream())
-    yk = torch.empty(N, C, 2 * H, 2 * H, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
+    big = Co % 8 == 0
+    if big:
+        wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems(Ci), device=dev, dtype=torch.bfloat16)
+        _lib.call("lv_deconv4s2_pack_weight_bf16", w.data_ptr(), wt.data_ptr(), Ci, Co, _lib.stream())
+    yk = torch.empty(N, Co, 2 * H, 2 * H, device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
 
     def kern(bm):
         _lib.call("lv_deconv4s2_fwd_bf16_tile", x.data_ptr(), wt.data_ptr(), b.data_ptr(), yk.data_ptr(),
-                  N, H, H, C, C, bm, _lib.stream())
-    for tag, fn in (("miopen", lambda: torch.nn.functional.conv_transpose2d(x, wcl, b.to(torch.bfloat16), 2, 1)),
-                    ("mfma", lambda: _Deconv4s2.apply(x, w, b)),
-                    ("gemm_bm128", lambda: kern(128)), ("gemm_bm256", lambda: kern(256))):
+                  N, H, H, Ci, Co, bm, _lib.stream())
+    runs = [("miopen", lambda: torch.nn.functional.conv_transpose2d(x, wcl, b.to(torch.bfloat16), 2, 1)),
+            ("mfma", lambda: _Deconv4s2.apply(x, w, b))]
+    if big:
+        runs += [("gemm_bm128", lambda: kern(128)), ("gemm_bm256", lambda: kern(256))]
+    for tag, fn in runs:
         for _ in range(5):
             fn()
         torch.cuda.synchronize()

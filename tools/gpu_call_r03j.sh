@@ -1,0 +1,5 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -k "mfma_deconv" -q --timeout 200 --timeout-method thread > gpurun_out/deconv_test.log 2>&1; echo "deconv tests rc=$?"; grep -E "passed|failed|Error|assert" gpurun_out/deconv_test.log | head -8
+timeout -k 10 300 python tools/deconv_bench.py > gpurun_out/deconv_bench.txt 2>&1; echo "deconv bench rc=$?"; grep -v amdgpu gpurun_out/deconv_bench.txt
+TIMEONLY=1 bash tools/gpu_train_prof.sh bf16_mfma
