@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--bias-grad", choices=["reduce", "gemv"], default="reduce",
                     help="stride-2 ConvTranspose2d bias gradient: strided reduction or a "
                          "ones-vector GEMM (nets.BIAS_GEMV)")
-    ap.add_argument("--deconv", choices=["transposed", "phase", "mfma"], default="transposed",
+    ap.add_argument("--deconv", choices=["transposed", "phase", "mfma"], default="mfma",
                     help="stride-2 ConvTranspose2d: MIOpen's transposed convolution, one 3x3 "
                          "convolution + pixel shuffle (nets.PHASE_DECONV), or the library's MFMA "
                          "kernel for bf16 channels-last (nets.MFMA_DECONV)")

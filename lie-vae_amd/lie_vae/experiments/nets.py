@@ -135,10 +135,11 @@ class BiasGemvConvTranspose2d(nn.ConvTranspose2d):
 
 
 PHASE_DECONV = False  # off: 10.5 vs 7.4 ms (bf16), 22.1 vs 15.2 ms (f32)
-# The stride-2 ConvTranspose2d forward on the library's MFMA kernel (lv_deconv4s2_fwd_bf16,
-# csrc/deconv.hip) when it runs in bf16 (autocast) on channels-last inputs; fp32 / NCHW /
-# unsupported shapes keep MIOpen.  The backward stays on PyTorch's convolution_backward.
-MFMA_DECONV = False
+# The stride-2 ConvTranspose2d forward on the library's MFMA kernels (lv_deconv4s2_fwd_bf16
+# and, for the RGB output layer, lv_deconv4s2_small_fwd_bf16; csrc/deconv.hip) when it runs
+# in bf16 (autocast) on channels-last inputs; fp32 / NCHW / unsupported shapes keep MIOpen.
+# Config 3 bf16: 7.41 -> 6.29 ms/step (dec5 forward 989 -> 77 us, dec2-4 2x faster).
+MFMA_DECONV = True
 
 
 class _Deconv4s2(torch.autograd.Function):
