@@ -215,6 +215,21 @@ size_t lv_deconv4s2_small_packed_weight_elems(int Cin);
 int lv_deconv4s2_small_pack_weight_bf16(const void* w, void* wq, int Cin, int Cout, void* stream);
 int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias, void* y,
                                 int64_t N, int H, int W, int Cin, int Cout, void* stream);
+/* Backward of the small-Cout layer: gx (dgrad; needs the weight repacked by
+ * lv_deconv4s2_small_pack_dgrad_weight_bf16 into lv_deconv4s2_small_dgrad_weight_elems(Cin)
+ * bf16), gw (bf16, the weight's (Cin, Cout, 4, 4) layout) and gb (fp32, optional, only with
+ * gw) from x and gy (bf16 channels-last).  gx or gw may be null to skip that product; gw
+ * needs ws of lv_deconv4s2_small_bwd_workspace_elems(...) floats.  Cin + 1 <= 256. */
+size_t lv_deconv4s2_small_dgrad_weight_elems(int Cin);
+int lv_deconv4s2_small_pack_dgrad_weight_bf16(const void* w, void* wd, int Cin, int Cout, void* stream);
+size_t lv_deconv4s2_small_bwd_workspace_elems(int64_t N, int H, int W, int Cin, int Cout);
+int lv_deconv4s2_small_bwd_bf16(const void* x, const void* gy, const void* wd, void* gx, void* gw, float* gb,
+                                float* ws, int64_t N, int H, int W, int Cin, int Cout, void* stream);
+/* out[c] = sum_p g[p, c] for a channels-last (P, C) bf16 tensor (the bias gradient of a
+ * convolution), C % 8 == 0; fixed-order (deterministic) two-pass sum, ws of
+ * lv_channel_sum_workspace_elems(P, C) floats. */
+size_t lv_channel_sum_workspace_elems(int64_t P, int C);
+int lv_channel_sum_bf16(const void* g, float* out, float* ws, int64_t P, int C, void* stream);
 /* Same with an explicit pixel-tile height (0 = the default, 128 or 256; A/B). */
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y,
                                int64_t N, int H, int W, int Cin, int Cout, int bm, void* stream);

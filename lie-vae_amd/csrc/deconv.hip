@@ -22,6 +22,8 @@
 // step's MFMAs run, then written to the other LDS buffer (row pitch 80 B: the 16-byte
 // fragment reads of 8 consecutive rows fall in distinct banks).  Epilogue: + bias, round
 // to bf16, stage the tile in LDS, 16-byte stores of whole 2·Cout-byte output rows.
+#include <algorithm>
+
 #include "lv_common.h"
 
 namespace lv {
@@ -370,6 +372,383 @@ __global__ __launch_bounds__(kSmallThreads) void deconv_small_kernel(DeconvSmall
   }
 }
 
+// ----------------------------------------------------- small-Cout decoder layer, backward
+// With the quad view of the forward (Y[quad, n] = sum_{nbr, c} X[quad + nbr - 1, c]
+// Wq[nbr, c, n], n = p·Cout + o), input pixel (a, b) meets quad (a - na + 1, b - nb + 1)
+// through neighbour nbr = (na, nb), so
+//   dgrad  gX[(a, b), c]   = sum_{nbr, n} gYq[(a, b) - nbr + 1, n] Wq[nbr, c, n]   (K = 9 x 16)
+//   wgrad  gWq[nbr, c, n]  = sum_{(a, b)} X[(a, b), c] gYq[(a, b) - nbr + 1, n]   (K = pixels)
+//   bias   gb[o]           = sum_{quads, p} gYq[quad, p·Cout + o]
+// Both kernels walk tiles of kBwTA x kBwTB input pixels of one image and stage the
+// (kBwTA + 2) x (kBwTB + 2) gradient quads around the tile in LDS as [quad][16] bf16.
+// dgrad writes 2·Cin bytes per pixel (the layer's HBM floor), wgrad reads them: each is a
+// single pass over the 2·N·H·W·Cin-byte activation.
+constexpr int kBwTA = 2, kBwTB = 32;                      // input pixels per tile (rows x cols)
+constexpr int kBwPix = kBwTA * kBwTB;                     // 64 = 4 MFMA tiles of 16 pixels
+constexpr int kBwQW = kBwTB + 2, kBwQuads = (kBwTA + 2) * kBwQW;   // 136 staged quads
+constexpr int kBwMaxCt = 16;                              // 16-channel tiles (Cin + 1 <= 256)
+constexpr int kDgThreads = 256, kWgThreads = 512;
+constexpr int kDgK = 160;                                 // dgrad K: 9 nbr x 16, padded to 5 x 32
+
+struct DeconvSmallBwdArgs {
+  const __hip_bfloat16* x;    // (N, H, W, Cin) channels-last
+  const __hip_bfloat16* gy;   // (N, 2H, 2W, Cout) channels-last
+  const __hip_bfloat16* wd;   // dgrad weight [nct·16][kDgK]
+  __hip_bfloat16* gx;         // (N, H, W, Cin) channels-last
+  float* part;                // wgrad partials [blocks][Cin·Cout·16 + 4·Cout]
+  int H, W, Cin, Cout, nct, tiles_w;
+  int tiles_img;              // tiles per image
+  int64_t ntiles;
+};
+
+// wd[c][nbr·16 + n] = Wq[nbr, c, n] (0 past Cin, past 4·Cout and for nbr = 9): the dgrad
+// A operand, 8 consecutive K of one channel per 16-byte load
+__global__ void deconv_small_pack_dgrad_kernel(const __hip_bfloat16* w, __hip_bfloat16* wd, int Cin, int Cout,
+                                               int rows) {
+  const int total = rows * kDgK;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i / kDgK, k = i - c * kDgK, nbr = k >> 4, n = k & 15;
+    const int p = n / Cout, o = n - p * Cout;
+    float v = 0.f;
+    if (c < Cin && p < 4 && nbr < 9) {
+      const int r = p >> 1, s = p & 1, di = nbr / 3 - 1, dj = nbr % 3 - 1;
+      if ((di == r - 1 || di == r) && (dj == s - 1 || dj == s))
+        v = __bfloat162float(w[((c * Cout + (n - p * Cout)) * 4 + 1 - 2 * di + r) * 4 + 1 - 2 * dj + s]);
+    }
+    (void)o;
+    wd[i] = __float2bfloat16(v);
+  }
+}
+
+// gYq of the quads around one tile: (kBwTA + 2) quad rows = 2 (kBwTA + 2) gradient rows,
+// each a contiguous run of 2 (kBwTB + 2) Cout values; zero outside the image.  load() takes
+// a tile's values into registers (issued a tile ahead, so the loads fly during the current
+// tile's MFMAs), store() writes them to the [quad][16] LDS image.
+template <int Co, int NTHR>
+struct QuadStage {
+  static constexpr int L = 2 * kBwQW * Co;
+  static constexpr int kN = 2 * (kBwTA + 2) * L;
+  static constexpr int kPer = (kN + NTHR - 1) / NTHR;
+  __hip_bfloat16 v[kPer];
+  __device__ __forceinline__ void load(const DeconvSmallBwdArgs& a, int64_t n_img, int a0, int b0, int tid) {
+    const int H2 = 2 * a.H, W2 = 2 * a.W;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * NTHR;
+      const int row = e / L, k = e - row * L;
+      const int qi = row >> 1, r = row & 1, pix = k / Co, o = k - pix * Co, qj = pix >> 1, s = pix & 1;
+      const int qa = a0 - 1 + qi, qb = b0 - 1 + qj;
+      v[i] = __float2bfloat16(0.f);
+      if (e < kN && qa >= 0 && qa < a.H && qb >= 0 && qb < a.W)
+        v[i] = a.gy[((n_img * H2 + 2 * qa + r) * W2 + 2 * qb + s) * Co + o];
+    }
+  }
+  __device__ __forceinline__ void store(__hip_bfloat16* qs, int tid) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * NTHR;
+      const int row = e / L, k = e - row * L;
+      const int qi = row >> 1, r = row & 1, pix = k / Co, o = k - pix * Co, qj = pix >> 1, s = pix & 1;
+      if (e < kN) qs[(qi * kBwQW + qj) * 16 + (2 * r + s) * Co + o] = v[i];
+    }
+  }
+};
+
+struct TileAt {
+  int64_t n;
+  int a0, b0;
+};
+__device__ __forceinline__ TileAt tile_at(const DeconvSmallBwdArgs& a, int64_t tile) {
+  const int64_t n = tile / a.tiles_img;
+  const int t = (int)(tile - n * a.tiles_img);
+  return TileAt{n, (t / a.tiles_w) * kBwTA, (t % a.tiles_w) * kBwTB};
+}
+
+// dgrad.  4 waves; wave w owns channel tiles w, w + 4, ... and keeps their weight
+// fragments in registers for the whole (persistent) block.  Per 16-pixel MFMA tile: five
+// 16-byte quad reads (B operand: K = 8 consecutive (nbr, n) of one pixel), five MFMAs per
+// channel tile (C rows = 4 consecutive channels per lane -> one 8-byte LDS store), then the
+// staged [64 pixels][Cin] tile leaves as 16-byte stores of whole pixel rows.
+template <int CO>
+__global__ __launch_bounds__(kDgThreads) void deconv_small_dgrad_kernel(DeconvSmallBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 sm[];
+  __hip_bfloat16* qs = sm;                               // [kBwQuads + 1][16], last = zeros
+  __hip_bfloat16* os = sm + (kBwQuads + 1) * 16;         // [kBwPix][pitch]
+  const int pitch = a.nct * 16 + 8;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  for (int i = tid; i < (kBwQuads + 1) * 2; i += kDgThreads)
+    reinterpret_cast<u32x4*>(qs)[i] = u32x4{0u, 0u, 0u, 0u};
+  constexpr int kPer = kBwMaxCt / 4;
+  bf16x8 wf[kPer][5];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int ct = wave + 4 * i;
+    if (ct < a.nct) {
+#pragma unroll
+      for (int st = 0; st < 5; ++st)
+        wf[i][st] = *reinterpret_cast<const bf16x8*>(a.wd + (ct * 16 + fr) * kDgK + st * 32 + g * 8);
+    }
+  }
+  // per lane: the quad offsets (elements) of its B fragments, relative to the pixel's quad
+  int boff[5];
+#pragma unroll
+  for (int st = 0; st < 5; ++st) {
+    const int nbr = 2 * st + (g >> 1);
+    const int na = nbr / 3, nb = nbr % 3;
+    boff[st] = nbr < 9 ? ((2 - na) * kBwQW + (2 - nb)) * 16 + 8 * (g & 1) : -1;
+  }
+  const int G8 = a.Cin / 8;
+  QuadStage<CO, kDgThreads> qst;
+  int64_t tile = blockIdx.x;
+  TileAt at = tile_at(a, tile);
+  if (tile < a.ntiles) qst.load(a, at.n, at.a0, at.b0, tid);
+  __syncthreads();  // the zeroed quad image
+  for (; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t n_img = at.n;
+    const int a0 = at.a0, b0 = at.b0;
+    qst.store(qs, tid);
+    __syncthreads();
+    if (tile + gridDim.x < a.ntiles) {  // next tile's quads in flight during this tile's MFMAs
+      at = tile_at(a, tile + gridDim.x);
+      qst.load(a, at.n, at.a0, at.b0, tid);
+    }
+#pragma unroll
+    for (int mt = 0; mt < kBwPix / 16; ++mt) {
+      const int ta = mt >> 1, tb = 16 * (mt & 1) + fr;
+      const int qbase = (ta * kBwQW + tb) * 16;
+      bf16x8 gf[5];
+#pragma unroll
+      for (int st = 0; st < 5; ++st)
+        gf[st] = *reinterpret_cast<const bf16x8*>(qs + (boff[st] >= 0 ? qbase + boff[st] : kBwQuads * 16));
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int ct = wave + 4 * i;
+        if (ct < a.nct) {
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int st = 0; st < 5; ++st) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i][st], gf[st], acc, 0, 0, 0);
+          __hip_bfloat16 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = __float2bfloat16(acc[j]);
+          *reinterpret_cast<uint2*>(os + (mt * 16 + fr) * pitch + ct * 16 + 4 * g) = *reinterpret_cast<const uint2*>(v);
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < kBwPix * G8; e += kDgThreads) {
+      const int px = e / G8, q = e - px * G8;
+      const int ia = a0 + px / kBwTB, ib = b0 + px % kBwTB;
+      if (ia < a.H && ib < a.W)
+        *reinterpret_cast<u32x4*>(a.gx + ((n_img * a.H + ia) * a.W + ib) * a.Cin + 8 * q) =
+            *reinterpret_cast<const u32x4*>(os + px * pitch + 8 * q);
+    }
+  }
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 8 K values (pixels) of one column from two 4-row transposed reads (ds_read_b64_tr_b16):
+// lane 4q + p of each 16-lane group names row q, columns 4p..4p+3 of a 4 x 16 block; lane i
+// of the group receives column i of the 4 rows.  `addr0`/`addr1` are this lane's element
+// addresses for the rows k0 + q and k0 + 4 + q.
+__device__ __forceinline__ bf16x8 tr_read8(const __hip_bfloat16* addr0, const __hip_bfloat16* addr1) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(as_lds(addr0)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(as_lds(addr1)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// wgrad + bias.  8 waves; wave w accumulates channel tiles w and w + 8 against all nine
+// neighbours (18 16x16 fp32 tiles).  Per tile row of 32 pixels (one MFMA K step): the A
+// operand (32 pixels x 16 channels of X, pixel-major in LDS) and the B operands (32 pixels
+// x 16 quad values per neighbour) are transposed reads.  Column Cin of the staged X is 1
+// on valid pixels, so channel row Cin of the centre neighbour accumulates the bias
+// gradient.  The block's sums leave once, in gw order, as fp32 partials.
+template <int CO>
+__global__ __launch_bounds__(kWgThreads) void deconv_small_wgrad_kernel(DeconvSmallBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 sm[];
+  __hip_bfloat16* qs = sm;                          // [kBwQuads][16]
+  __hip_bfloat16* xs = sm + kBwQuads * 16;          // [kBwPix][xpitch]
+  const int xpitch = a.nct * 16 + 8;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
+  constexpr int kPer = kBwMaxCt / 8;
+  f32x4 acc[kPer][9];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i)
+#pragma unroll
+    for (int nb = 0; nb < 9; ++nb) acc[i][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int G8 = a.nct * 2;   // 8-channel pieces per staged pixel
+  constexpr int kXPer = kBwPix * 2 * kBwMaxCt / kWgThreads;
+  u32x4 xv[kXPer];
+  auto load_x = [&](const TileAt& t) {
+#pragma unroll
+    for (int i = 0; i < kXPer; ++i) {
+      const int e = tid + i * kWgThreads;
+      const int px = e / G8, c = 8 * (e - px * G8);
+      const int ia = t.a0 + px / kBwTB, ib = t.b0 + px % kBwTB;
+      xv[i] = u32x4{0u, 0u, 0u, 0u};
+      if (e < kBwPix * G8 && ia < a.H && ib < a.W) {
+        if (c < a.Cin)
+          xv[i] = *reinterpret_cast<const u32x4*>(a.x + ((t.n * a.H + ia) * a.W + ib) * a.Cin + c);
+        else if (c == a.Cin)
+          xv[i][0] = 0x3f80u;  // bf16 1.0 in element 0 (channel Cin)
+      }
+    }
+  };
+  QuadStage<CO, kWgThreads> qst;
+  int64_t tile = blockIdx.x;
+  TileAt at = tile_at(a, tile);
+  if (tile < a.ntiles) {
+    qst.load(a, at.n, at.a0, at.b0, tid);
+    load_x(at);
+  }
+  for (; tile < a.ntiles; tile += gridDim.x) {
+    qst.store(qs, tid);
+#pragma unroll
+    for (int i = 0; i < kXPer; ++i) {
+      const int e = tid + i * kWgThreads;
+      const int px = e / G8, c = 8 * (e - px * G8);
+      if (e < kBwPix * G8) *reinterpret_cast<u32x4*>(xs + px * xpitch + c) = xv[i];
+    }
+    __syncthreads();
+    if (tile + gridDim.x < a.ntiles) {  // next tile in flight during this tile's MFMAs
+      at = tile_at(a, tile + gridDim.x);
+      qst.load(a, at.n, at.a0, at.b0, tid);
+      load_x(at);
+    }
+#pragma unroll
+    for (int ks = 0; ks < kBwTA; ++ks) {
+      bf16x8 af[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int ct = wave + 8 * i;
+        if (ct < a.nct) {
+          const __hip_bfloat16* base = xs + (ks * kBwTB + 8 * g + q4) * xpitch + ct * 16 + 4 * p4;
+          af[i] = tr_read8(base, base + 4 * xpitch);
+        }
+      }
+#pragma unroll
+      for (int nbr = 0; nbr < 9; ++nbr) {
+        const int na = nbr / 3, nb = nbr % 3;
+        const __hip_bfloat16* base = qs + ((ks - na + 2) * kBwQW + 8 * g + q4 - nb + 2) * 16 + 4 * p4;
+        const bf16x8 bfr = tr_read8(base, base + 4 * 16);
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+          const int ct = wave + 8 * i;
+          if (ct < a.nct) acc[i][nbr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][nbr], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // C: column n = fr -> (phase p, channel o); rows c = ct·16 + 4g + j
+  constexpr int Co = CO;
+  const int p = fr / Co, o = fr - p * Co;
+  if (p >= 4) return;
+  const int r = p >> 1, s = p & 1;
+  float* part = a.part + (int64_t)blockIdx.x * ((int64_t)a.Cin * Co * 16 + 4 * Co);
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int ct = wave + 8 * i;
+    if (ct >= a.nct) continue;
+#pragma unroll
+    for (int nbr = 0; nbr < 9; ++nbr) {
+      const int di = nbr / 3 - 1, dj = nbr % 3 - 1;
+      if (!((di == r - 1 || di == r) && (dj == s - 1 || dj == s))) continue;
+      const int ku = 1 - 2 * di + r, kv = 1 - 2 * dj + s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ct * 16 + 4 * g + j;
+        if (c < a.Cin)
+          part[((c * Co + o) * 4 + ku) * 4 + kv] = acc[i][nbr][j];
+        else if (c == a.Cin && nbr == 4)
+          part[a.Cin * Co * 16 + p * Co + o] = acc[i][nbr][j];
+      }
+    }
+  }
+}
+
+// out[e] = sum_{b < nblk} part[b·stride + e] for e < E, in a fixed order: four slices
+// (b mod 4), each an 8-way unrolled sum (8 independent loads in flight per thread), then
+// the slices added in order.  64 consecutive outputs per block: coalesced 256-byte rows.
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* part, int nblk, int64_t stride, int E,
+                                                           float* out) {
+  __shared__ float red[4][64];
+  const int t = (int)threadIdx.x, el = t & 63, sl = t >> 6;
+  const int e = blockIdx.x * 64 + el;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < E) {
+    int b = sl;
+    for (; b + 28 < nblk; b += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(b + 4 * u) * stride + e];
+    }
+    for (; b < nblk; b += 4) acc[0] += part[(int64_t)b * stride + e];
+  }
+  red[sl][el] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (sl == 0 && e < E) out[e] = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+}
+
+// gw (bf16, the weight's layout) and gb[o] = sum_p of the reduced wgrad sums
+__global__ void deconv_small_wgrad_finish_kernel(const float* red, int Cin, int Cout, __hip_bfloat16* gw, float* gb) {
+  const int nw = Cin * Cout * 16;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nw) {
+    gw[e] = __float2bfloat16(red[e]);
+  } else if (e < nw + Cout && gb) {
+    const int o = e - nw;
+    gb[o] = ((red[nw + o] + red[nw + Cout + o]) + red[nw + 2 * Cout + o]) + red[nw + 3 * Cout + o];
+  }
+}
+
+// ----------------------------------------------------- per-channel sum (bias gradient)
+// out[c] = sum_p g[p, c] over a channels-last (P, C) bf16 tensor, C % 8 == 0: each block
+// sums a contiguous row range (thread = 8 channels x every R-th row), a fixed-order LDS
+// combine, then a second kernel adds the per-block partials in block order.
+constexpr int kCsThreads = 256, kCsMaxBlocks = 1024;
+
+__global__ __launch_bounds__(kCsThreads) void channel_sum_part_kernel(const __hip_bfloat16* g, float* part, int64_t P,
+                                                                      int C, int64_t rows_per_blk) {
+  __shared__ float red[kCsThreads * 8];
+  const int G = C / 8, R = kCsThreads / G;
+  const int tid = (int)threadIdx.x, cg = tid % G, rr = tid / G;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk, r1 = min(P, r0 + rows_per_blk);
+  if (rr < R) {
+    auto add = [&](const u32x4 v) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[2 * e] += __uint_as_float(v[e] << 16);
+        s[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+      }
+    };
+    int64_t row = r0 + rr;
+    for (; row + 3 * R < r1; row += 4 * R) {  // four rows in flight
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(g + (row + u * R) * C + 8 * cg);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u]);
+    }
+    for (; row < r1; row += R) add(*reinterpret_cast<const u32x4*>(g + row * C + 8 * cg));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[rr * C + 8 * cg + e] = s[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kCsThreads) {
+    float t = 0.f;
+    for (int k = 0; k < R; ++k) t += red[k * C + c];
+    part[(int64_t)blockIdx.x * C + c] = t;
+  }
+}
+
 }  // namespace
 }  // namespace lv
 
@@ -451,6 +830,120 @@ int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias
   hipLaunchKernelGGL(deconv_small_kernel, dim3(th * tw, (unsigned)N), dim3(kSmallThreads), 0,
                      (hipStream_t)stream, a);
   LV_RETURN_LAUNCH("deconv_small_kernel");
+}
+
+static int small_bwd_nct(int Cin) { return (Cin + 1 + 15) / 16; }  // + the bias "ones" channel
+
+size_t lv_deconv4s2_small_dgrad_weight_elems(int Cin) { return (size_t)small_bwd_nct(Cin) * 16 * kDgK; }
+
+int lv_deconv4s2_small_pack_dgrad_weight_bf16(const void* w, void* wd, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(w && wd, "null pointer");
+  LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0 && small_bwd_nct(Cin) <= kBwMaxCt,
+               "Cin must be a positive multiple of 8 below %d (got %d)", 16 * kBwMaxCt, Cin);
+  LV_CHECK_ARG(Cout >= 1 && Cout <= kSmallMaxCout, "Cout must be in [1, %d] (got %d)", kSmallMaxCout, Cout);
+  const int rows = small_bwd_nct(Cin) * 16;
+  hipLaunchKernelGGL(deconv_small_pack_dgrad_kernel, dim3(ceil_div(rows * kDgK, 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const __hip_bfloat16*)w, (__hip_bfloat16*)wd, Cin, Cout, rows);
+  LV_RETURN_LAUNCH("deconv_small_pack_dgrad_kernel");
+}
+
+constexpr int kWgMaxBlocks = 512;  // wgrad partial slabs (workspace bound)
+static int small_wgrad_blocks(int64_t ntiles) { return (int)std::min<int64_t>(ntiles, kWgMaxBlocks); }
+
+// resident blocks of a persistent kernel on this device (all CUs x its occupancy), cached
+static int resident_blocks(const void* kern, int threads, size_t lds) {
+  static const void* keys[16];
+  static int vals[16];
+  static int used = 0;
+  for (int i = 0; i < used; ++i)
+    if (keys[i] == kern) return vals[i];
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) per_cu = 1;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  const int v = std::max(1, per_cu) * std::max(1, cus);
+  if (used < 16) { keys[used] = kern; vals[used] = v; ++used; }
+  return v;
+}
+
+size_t lv_deconv4s2_small_bwd_workspace_elems(int64_t N, int H, int W, int Cin, int Cout) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  const int64_t ntiles = N * ((H + kBwTA - 1) / kBwTA) * ((W + kBwTB - 1) / kBwTB);
+  return ((size_t)small_wgrad_blocks(ntiles) + 1) * ((size_t)Cin * Cout * 16 + 4 * (size_t)Cout);
+}
+
+int lv_deconv4s2_small_bwd_bf16(const void* x, const void* gy, const void* wd, void* gx, void* gw, float* gb,
+                                float* ws, int64_t N, int H, int W, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
+  LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0 && small_bwd_nct(Cin) <= kBwMaxCt,
+               "Cin must be a positive multiple of 8 below %d (got %d)", 16 * kBwMaxCt, Cin);
+  LV_CHECK_ARG(Cout >= 1 && Cout <= kSmallMaxCout, "Cout must be in [1, %d] (got %d)", kSmallMaxCout, Cout);
+  LV_CHECK_ARG(x && gy, "null pointer");
+  LV_CHECK_ARG(!gx || wd, "gx needs the packed dgrad weight");
+  LV_CHECK_ARG(!gw || ws, "gw needs the workspace");
+  hipStream_t st = (hipStream_t)stream;
+  const int tw = (W + kBwTB - 1) / kBwTB, th = (H + kBwTA - 1) / kBwTA;
+  const int64_t ntiles = N * th * tw;
+  DeconvSmallBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)gy, (const __hip_bfloat16*)wd,
+                       (__hip_bfloat16*)gx, ws, H, W, Cin, Cout, small_bwd_nct(Cin), tw, th * tw, ntiles};
+  const int nw = Cin * Cout * 16;
+  if (ntiles == 0) {  // empty batch: zero gradients
+    if (gw) LV_CHECK_HIP(hipMemsetAsync(gw, 0, (size_t)nw * 2, st));
+    if (gb) LV_CHECK_HIP(hipMemsetAsync(gb, 0, (size_t)Cout * 4, st));
+    return LV_OK;
+  }
+  if (gx) {
+    const size_t lds = ((size_t)(kBwQuads + 1) * 16 + (size_t)kBwPix * (a.nct * 16 + 8)) * 2;
+    auto k = Cout == 1 ? deconv_small_dgrad_kernel<1> : Cout == 2 ? deconv_small_dgrad_kernel<2>
+           : Cout == 3 ? deconv_small_dgrad_kernel<3> : deconv_small_dgrad_kernel<4>;
+    const int blocks = (int)std::min<int64_t>(ntiles, resident_blocks((const void*)k, kDgThreads, lds));
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kDgThreads), lds, st, a);
+    LV_CHECK_LAUNCH("deconv_small_dgrad_kernel");
+  }
+  LV_CHECK_ARG(gw || !gb, "gb is computed with gw");
+  if (gw) {
+    const size_t lds = ((size_t)kBwQuads * 16 + (size_t)kBwPix * (a.nct * 16 + 8)) * 2;
+    auto k = Cout == 1 ? deconv_small_wgrad_kernel<1> : Cout == 2 ? deconv_small_wgrad_kernel<2>
+           : Cout == 3 ? deconv_small_wgrad_kernel<3> : deconv_small_wgrad_kernel<4>;
+    const int blocks = std::min(small_wgrad_blocks(ntiles), resident_blocks((const void*)k, kWgThreads, lds));
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kWgThreads), lds, st, a);
+    LV_CHECK_LAUNCH("deconv_small_wgrad_kernel");
+    const int E = nw + 4 * Cout;
+    float* red = ws + (size_t)blocks * E;
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(ceil_div(E, 64)), dim3(256), 0, st, ws, blocks, (int64_t)E, E, red);
+    LV_CHECK_LAUNCH("sum_partials_kernel");
+    hipLaunchKernelGGL(deconv_small_wgrad_finish_kernel, dim3(ceil_div(nw + Cout, 256)), dim3(256), 0, st, red, Cin,
+                       Cout, (__hip_bfloat16*)gw, gb);
+    LV_RETURN_LAUNCH("deconv_small_wgrad_finish_kernel");
+  }
+  return LV_OK;
+}
+
+size_t lv_channel_sum_workspace_elems(int64_t P, int C) {
+  if (P <= 0 || C <= 0) return 0;
+  return ((size_t)std::min<int64_t>(kCsMaxBlocks, (P + 255) / 256) + 1) * C;
+}
+
+int lv_channel_sum_bf16(const void* g, float* out, float* ws, int64_t P, int C, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(P >= 0 && C > 0 && C % 8 == 0 && C / 8 <= kCsThreads, "C must be a multiple of 8 in [8, %d] (got %d)",
+               8 * kCsThreads, C);
+  LV_CHECK_ARG(out, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (P == 0) {
+    LV_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)C * 4, st));
+    return LV_OK;
+  }
+  LV_CHECK_ARG(g && ws, "null pointer");
+  const int nblk = (int)std::min<int64_t>(kCsMaxBlocks, (P + 255) / 256);
+  const int64_t rows = (P + nblk - 1) / nblk;
+  hipLaunchKernelGGL(channel_sum_part_kernel, dim3(nblk), dim3(kCsThreads), 0, st, (const __hip_bfloat16*)g, ws, P, C,
+                     rows);
+  LV_CHECK_LAUNCH("channel_sum_part_kernel");
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, st, ws, nblk, (int64_t)C, C, out);
+  LV_RETURN_LAUNCH("sum_partials_kernel");
 }
 
 }  // extern "C"

@@ -34,6 +34,25 @@ void clear_error();
     return LV_OK;                                                             \
   } while (0)
 
+// Like LV_RETURN_LAUNCH, but falls through on success (more work follows).
+#define LV_CHECK_LAUNCH(kname)                                                \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess) {                                                   \
+      ::lv::set_error("%s: launch failed: %s", kname, hipGetErrorString(e_)); \
+      return LV_ERR_HIP;                                                      \
+    }                                                                         \
+  } while (0)
+
+#define LV_CHECK_HIP(call)                                                    \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      ::lv::set_error("%s: %s", #call, hipGetErrorString(e_));                \
+      return LV_ERR_HIP;                                                      \
+    }                                                                         \
+  } while (0)
+
 // ---------------------------------------------------------------- static_for
 template <class F, int... Is>
 __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {

@@ -142,11 +142,25 @@ PHASE_DECONV = False  # off: 10.5 vs 7.4 ms (bf16), 22.1 vs 15.2 ms (f32)
 MFMA_DECONV = True
 
 
+def _channel_sum(g):
+    """sum over (n, h, w) of a channels-last bf16 (N, C, H, W) gradient: the library's
+    fixed-order per-channel sum (lv_channel_sum_bf16), fp32."""
+    from .. import _lib
+    C = g.shape[1]
+    P = g.numel() // C
+    out = torch.empty(C, device=g.device, dtype=torch.float32)
+    ws = torch.empty(max(1, _lib.load().lv_channel_sum_workspace_elems(P, C)), device=g.device,
+                     dtype=torch.float32)
+    _lib.call("lv_channel_sum_bf16", g.data_ptr(), out.data_ptr(), ws.data_ptr(), P, C, _lib.stream())
+    return out
+
+
 class _Deconv4s2(torch.autograd.Function):
     """y = conv_transpose2d(x, w, b, stride 2, padding 1), k = 4: forward on the MFMA
-    kernel (x, w bf16; b fp32 added before the bf16 rounding), backward through
-    aten.convolution_backward on the saved bf16 operands (what MIOpen computes for the
-    plain layer)."""
+    kernels (x, w bf16; b fp32 added before the bf16 rounding).  Backward: for Cout <= 4
+    the library's quad-view dgrad / wgrad / bias kernels (lv_deconv4s2_small_bwd_bf16);
+    otherwise aten.convolution_backward on the saved bf16 operands (what MIOpen computes
+    for the plain layer) for gx, gw and the library's per-channel sum for gb."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -170,11 +184,35 @@ class _Deconv4s2(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        from .. import _lib
         x, w = ctx.saved_tensors
-        gx, gw, gb = torch.ops.aten.convolution_backward(
-            gy.to(torch.bfloat16), x, w, [w.shape[1]] if ctx.has_bias else None, [2, 2], [1, 1],
-            [1, 1], True, [0, 0], 1, [True, True, ctx.has_bias])
-        return gx, gw, (gb.float() if ctx.has_bias else None)
+        N, Cin, H, W = x.shape
+        Cout = w.shape[1]
+        gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        need_x, need_w, need_b = ctx.needs_input_grad
+        need_b = need_b and ctx.has_bias
+        if Cout <= 4:
+            lib, st = _lib.load(), _lib.stream()
+            gx = wd = gw = gb = ws = None
+            if need_x:
+                wd = torch.empty(lib.lv_deconv4s2_small_dgrad_weight_elems(Cin), device=x.device,
+                                 dtype=torch.bfloat16)
+                _lib.call("lv_deconv4s2_small_pack_dgrad_weight_bf16", w.data_ptr(), wd.data_ptr(),
+                          Cin, Cout, st)
+                gx = torch.empty_like(x, memory_format=torch.channels_last)
+            if need_w or need_b:
+                gw = torch.empty_like(w)
+                gb = torch.empty(Cout, device=x.device, dtype=torch.float32) if need_b else None
+                ws = torch.empty(max(1, lib.lv_deconv4s2_small_bwd_workspace_elems(N, H, W, Cin, Cout)),
+                                 device=x.device, dtype=torch.float32)
+            _lib.call("lv_deconv4s2_small_bwd_bf16", x.data_ptr(), gy.data_ptr(),
+                      None if wd is None else wd.data_ptr(), None if gx is None else gx.data_ptr(),
+                      None if gw is None else gw.data_ptr(), None if gb is None else gb.data_ptr(),
+                      None if ws is None else ws.data_ptr(), N, H, W, Cin, Cout, st)
+            return gx, (gw if need_w else None), gb
+        gx, gw, _ = torch.ops.aten.convolution_backward(
+            gy, x, w, None, [2, 2], [1, 1], [1, 1], True, [0, 0], 1, [need_x, need_w, False])
+        return gx, gw, (_channel_sum(gy) if need_b else None)
 
 
 class MfmaConvTranspose2d(nn.ConvTranspose2d):

@@ -561,3 +561,36 @@ def test_mfma_deconv_module_under_autocast(gpu_device):
     torch.testing.assert_close(xs[0].grad, xs[1].grad, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(m.weight.grad, r.weight.grad, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(m.bias.grad, r.bias.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(3, 200, 3, 32, 32), (2, 40, 1, 9, 21), (2, 200, 4, 17, 16),
+                                           (1, 248, 3, 5, 40), (2, 64, 200, 7, 9)])
+def test_mfma_deconv_backward_matches_autograd(gpu_device, N, Cin, Cout, H, W):
+    """_Deconv4s2.backward: for Cout <= 4 lv_deconv4s2_small_bwd_bf16 (dgrad, wgrad and
+    bias from the quad view; csrc/deconv.hip), otherwise MIOpen's gx/gw with the library's
+    per-channel bias sum (lv_channel_sum_bf16) -- against float64 autograd of
+    conv_transpose2d on the same bf16-rounded x, w and gy.  Tolerance: the library's gx, gw
+    are rounded to bf16 once (|err| <= 2^-8 |ref| + 1e-3 rms); MIOpen's (Cout > 4) measure up
+    to ~2% off (its bf16 split-K partials), checked at 2^-5 |ref| + 1e-2 rms; gb is fp32
+    (1e-4 relative + 1e-5 rms)."""
+    from lie_vae.experiments.nets import _Deconv4s2
+    g = torch.Generator().manual_seed(N * 7 + Cin + Cout + H * W)
+    x = torch.randn(N, Cin, H, W, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cin, Cout, 4, 4, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g)
+    gy = torch.randn(N, Cout, 2 * H, 2 * W, generator=g).to(torch.bfloat16)
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.conv_transpose2d(xr, wr, br, 2, 1).backward(gy.double())
+    xd = x.to(gpu_device).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wd = w.to(gpu_device).requires_grad_(True)
+    bd = b.to(gpu_device).requires_grad_(True)
+    _Deconv4s2.apply(xd, wd, bd).backward(gy.to(gpu_device).contiguous(memory_format=torch.channels_last))
+    rel_l, abs_l = (2.0 ** -8, 1e-3) if Cout <= 4 else (2.0 ** -5, 1e-2)
+    for name, got, ref, rel, absr in (("gx", xd.grad, xr.grad, rel_l, abs_l),
+                                      ("gw", wd.grad, wr.grad, rel_l, abs_l),
+                                      ("gb", bd.grad, br.grad, 1e-4, 1e-5)):
+        assert got.shape == ref.shape, name
+        gd = got.double().cpu()
+        rms = ref.square().mean().sqrt()
+        bad = (gd - ref).abs() > rel * ref.abs() + absr * rms
+        assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
