@@ -230,6 +230,22 @@ int lv_deconv4s2_small_bwd_bf16(const void* x, const void* gy, const void* wd, v
  * lv_channel_sum_workspace_elems(P, C) floats. */
 size_t lv_channel_sum_workspace_elems(int64_t P, int C);
 int lv_channel_sum_bf16(const void* g, float* out, float* ws, int64_t P, int C, void* stream);
+/* ---- encoder BatchNorm2d + LeakyReLU (csrc/bn.hip; reference nets.py:33-57) ------------
+ * x: channels-last (P, C) bf16, P = N·H·W.  Supported when lv_bn_supported(P, C): C >= 8,
+ * C / gcd(C, 8) <= 256 and P a multiple of 8 / gcd(C, 8).  training = 1: batch statistics
+ * (biased variance), save_mean / save_invstd written, running stats (may be null) updated
+ * with `momentum` (unbiased variance), as torch.nn.BatchNorm2d; training = 0: the running
+ * statistics normalise.  y = z > 0 ? z : slope·z, z = gamma·(x - mean)·invstd + beta
+ * (gamma / beta null = 1 / 0).  ws: lv_bn_workspace_elems(P, C) floats.  Deterministic. */
+int lv_bn_supported(int64_t P, int C);
+size_t lv_bn_workspace_elems(int64_t P, int C);
+int lv_bn_lrelu_fwd_bf16(const void* x, const float* gamma, const float* beta, float* running_mean,
+                         float* running_var, int training, float momentum, float eps, float slope, void* y,
+                         float* save_mean, float* save_invstd, float* ws, int64_t P, int C, void* stream);
+/* Backward of the training-mode forward: gx (bf16), ggamma / gbeta (fp32, may be null). */
+int lv_bn_lrelu_bwd_bf16(const void* g, const void* x, const float* gamma, const float* beta,
+                         const float* save_mean, const float* save_invstd, float slope, void* gx,
+                         float* ggamma, float* gbeta, float* ws, int64_t P, int C, void* stream);
 /* Same with an explicit pixel-tile height (0 = the default, 128 or 256; A/B). */
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y,
                                int64_t N, int H, int W, int Cin, int Cout, int bm, void* stream);

@@ -20,6 +20,7 @@ _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _I = ctypes.c_int
 _SZ = ctypes.c_size_t
+_F = ctypes.c_float
 
 # name -> argtypes (restype int unless noted)
 _SIGS = {
@@ -72,15 +73,18 @@ _SIGS["lv_deconv4s2_small_fwd_bf16"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _P
 _SIGS["lv_deconv4s2_small_pack_dgrad_weight_bf16"] = [_P, _P, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _I, _I, _P]
 _SIGS["lv_channel_sum_bf16"] = [_P, _P, _P, _I64, _I, _P]
+_SIGS["lv_bn_lrelu_fwd_bf16"] = [_P, _P, _P, _P, _P, _I, _F, _F, _F, _P, _P, _P, _P, _I64, _I, _P]
+_SIGS["lv_bn_lrelu_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I64, _I, _P]
 _RESTYPES = {"lv_group_action_bwd_workspace": _SZ, "lv_last_error": ctypes.c_char_p,
              "lv_deconv4s2_packed_weight_elems": _SZ, "lv_deconv4s2_small_packed_weight_elems": _SZ,
              "lv_deconv4s2_small_dgrad_weight_elems": _SZ, "lv_deconv4s2_small_bwd_workspace_elems": _SZ,
-             "lv_channel_sum_workspace_elems": _SZ}
+             "lv_channel_sum_workspace_elems": _SZ, "lv_bn_workspace_elems": _SZ}
 _SIGS_EXTRA = {"lv_group_action_bwd_workspace": [_I64, _I, _I, _I], "lv_last_error": [],
                "lv_deconv4s2_packed_weight_elems": [_I], "lv_deconv4s2_small_packed_weight_elems": [_I],
                "lv_deconv4s2_small_dgrad_weight_elems": [_I],
                "lv_deconv4s2_small_bwd_workspace_elems": [_I64, _I, _I, _I, _I],
-               "lv_channel_sum_workspace_elems": [_I64, _I]}
+               "lv_channel_sum_workspace_elems": [_I64, _I],
+               "lv_bn_supported": [_I64, _I], "lv_bn_workspace_elems": [_I64, _I]}
 
 EXPORTED = sorted(list(_SIGS) + list(_SIGS_EXTRA))
 

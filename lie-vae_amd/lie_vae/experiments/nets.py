@@ -17,6 +17,7 @@ plain convolutions (A/B).
 """
 import torch
 from torch import nn
+from torch.nn import functional as F
 
 GEMM_LAYERS = True
 
@@ -85,6 +86,10 @@ class GemmConv2d(nn.Conv2d):
 #              10.0 vs 7.7 ms -- without its bias MIOpen picks slower deconv solutions)
 NATIVE_BN = True
 BIAS_GEMV = False
+# FUSED_BN_ACT: the encoder's BatchNorm2d + LeakyReLU pair as FusedBatchNormLeakyReLU (the
+# library's deterministic bf16 channels-last kernels, csrc/bn.hip) + an Identity placeholder
+# (same Sequential indices and state_dict keys).
+FUSED_BN_ACT = True
 
 
 class NativeBatchNorm2d(nn.BatchNorm2d):
@@ -100,6 +105,108 @@ class NativeBatchNorm2d(nn.BatchNorm2d):
             return super().forward(x)
         finally:
             torch.backends.cudnn.enabled = prev
+
+
+class _BnLeakyReLU(torch.autograd.Function):
+    """Training-mode BatchNorm2d + LeakyReLU on a channels-last bf16 activation through the
+    library (lv_bn_lrelu_fwd_bf16 / lv_bn_lrelu_bwd_bf16, csrc/bn.hip): batch statistics,
+    running-stat update, y = lrelu(gamma·xhat + beta) in one stats pass + one apply pass;
+    backward = one reduce pass + one apply pass.  x is saved (not y): z is recomputed."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, slope):
+        from .. import _lib
+        N, C, H, W = x.shape
+        P = N * H * W
+        dev = x.device
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        mean = torch.empty(C, device=dev, dtype=torch.float32)
+        invstd = torch.empty(C, device=dev, dtype=torch.float32)
+        ws = torch.empty(_lib.load().lv_bn_workspace_elems(P, C), device=dev, dtype=torch.float32)
+        _lib.call("lv_bn_lrelu_fwd_bf16", x.data_ptr(), _lib.ptr(weight), _lib.ptr(bias),
+                  _lib.ptr(running_mean), _lib.ptr(running_var), 1, momentum, eps, slope,
+                  y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), P, C, _lib.stream())
+        ctx.save_for_backward(x, weight, bias, mean, invstd)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _lib
+        x, weight, bias, mean, invstd = ctx.saved_tensors
+        N, C, H, W = x.shape
+        P = N * H * W
+        g = g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gx = torch.empty_like(x, memory_format=torch.channels_last)
+        gw = torch.empty_like(weight) if weight is not None else None
+        gb = torch.empty_like(bias) if bias is not None else None
+        ws = torch.empty(_lib.load().lv_bn_workspace_elems(P, C), device=x.device, dtype=torch.float32)
+        _lib.call("lv_bn_lrelu_bwd_bf16", g.data_ptr(), x.data_ptr(), _lib.ptr(weight), _lib.ptr(bias),
+                  mean.data_ptr(), invstd.data_ptr(), ctx.slope, gx.data_ptr(), _lib.ptr(gw), _lib.ptr(gb),
+                  ws.data_ptr(), P, C, _lib.stream())
+        return gx, gw, gb, None, None, None, None, None
+
+
+class FusedBatchNormLeakyReLU(nn.BatchNorm2d):
+    """BatchNorm2d(c) followed by LeakyReLU(slope) (the ConvNetBN pair, reference
+    nets.py:33-57) in one module with BatchNorm2d's parameters, buffers and state_dict.
+    Training-mode bf16 channels-last inputs on the GPU run the library's fused kernels;
+    everything else (eval, fp32, NCHW, unsupported C) is BatchNorm2d + leaky_relu."""
+
+    def __init__(self, num_features, negative_slope=0.2, **kw):
+        super().__init__(num_features, **kw)
+        self.negative_slope = negative_slope
+
+    def _fused_ok(self, x):
+        from .. import _lib
+        if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and _cl(x)
+                and self.training and self.track_running_stats and self.momentum is not None):
+            return False
+        N, C, H, W = x.shape
+        return N * H * W > 1 and bool(_lib.load().lv_bn_supported(N * H * W, C))
+
+    def forward(self, x):
+        if not self._fused_ok(x):
+            return F.leaky_relu(super().forward(x), self.negative_slope)
+        self.num_batches_tracked.add_(1)
+        return _BnLeakyReLU.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                  float(self.momentum), float(self.eps), float(self.negative_slope))
+
+
+class SyncBatchNormLeakyReLU(nn.SyncBatchNorm):
+    """SyncBatchNorm (global-batch statistics) + LeakyReLU: what to_sync_batchnorm turns a
+    FusedBatchNormLeakyReLU into for data-parallel training (same state_dict keys)."""
+
+    def __init__(self, num_features, negative_slope=0.2, **kw):
+        super().__init__(num_features, **kw)
+        self.negative_slope = negative_slope
+
+    def forward(self, x):
+        return F.leaky_relu(super().forward(x), self.negative_slope)
+
+
+def to_sync_batchnorm(module, process_group=None):
+    """torch.nn.SyncBatchNorm.convert_sync_batchnorm that keeps the activation of the fused
+    BatchNorm + LeakyReLU layers (FusedBatchNormLeakyReLU -> SyncBatchNormLeakyReLU)."""
+    if isinstance(module, FusedBatchNormLeakyReLU):
+        out = SyncBatchNormLeakyReLU(module.num_features, module.negative_slope, eps=module.eps,
+                                     momentum=module.momentum, affine=module.affine,
+                                     track_running_stats=module.track_running_stats,
+                                     process_group=process_group)
+        if module.affine:
+            with torch.no_grad():
+                out.weight = module.weight
+                out.bias = module.bias
+        out.running_mean = module.running_mean
+        out.running_var = module.running_var
+        out.num_batches_tracked = module.num_batches_tracked
+        out.training = module.training
+        return out
+    if isinstance(module, nn.modules.batchnorm._BatchNorm) and not isinstance(module, nn.SyncBatchNorm):
+        return nn.SyncBatchNorm.convert_sync_batchnorm(module, process_group)
+    for name, child in module.named_children():
+        module.add_module(name, to_sync_batchnorm(child, process_group))
+    return module
 
 
 class _BiasAdd(torch.autograd.Function):
@@ -318,9 +425,12 @@ def _down_stack(in_dims, hidden, out_dims, batch_norm):
     layers, c = [], in_dims
     for i, width in enumerate([hidden, hidden * 2, hidden * 4, hidden * 8]):
         layers.append(nn.Conv2d(c, width, 4, 2, 1))
-        if batch_norm:
-            layers.append(_bn(width))
-        layers.append(nn.LeakyReLU(0.2, inplace=True))
+        if batch_norm and FUSED_BN_ACT:
+            layers += [FusedBatchNormLeakyReLU(width, 0.2), nn.Identity()]
+        else:
+            if batch_norm:
+                layers.append(_bn(width))
+            layers.append(nn.LeakyReLU(0.2, inplace=True))
         c = width
     layers += [_conv(c, out_dims, 4, 1, 0), Flatten()]
     return layers

@@ -152,7 +152,8 @@ class DPTrainer:
                  control=None, control_p=1, selective_clip=False, nan_check=False,
                  amp_dtype=None, graph=False, sync_bn=False):
         if sync_bn and dist.is_initialized() and dist.get_world_size(group) > 1:
-            model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model, process_group=group)
+            from .nets import to_sync_batchnorm
+            model = to_sync_batchnorm(model, process_group=group)
         self.model = model
         self.amp_dtype = amp_dtype
         self.clip = clip_grads

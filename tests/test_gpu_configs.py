@@ -594,3 +594,61 @@ def test_mfma_deconv_backward_matches_autograd(gpu_device, N, Cin, Cout, H, W):
         rms = ref.square().mean().sqrt()
         bad = (gd - ref).abs() > rel * ref.abs() + absr * rms
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
+
+
+@pytest.mark.parametrize("N,C,H,W", [(64, 50, 32, 32), (16, 100, 16, 16), (32, 200, 8, 8), (64, 400, 4, 4),
+                                     (3, 24, 5, 7), (2, 12, 3, 3), (2, 6, 4, 4)])
+def test_fused_bn_leaky_relu_matches_float64(gpu_device, N, C, H, W):
+    """FusedBatchNormLeakyReLU in training mode on a bf16 channels-last activation
+    (lv_bn_lrelu_fwd_bf16 / lv_bn_lrelu_bwd_bf16, csrc/bn.hip; C = 6 takes the
+    BatchNorm2d + leaky_relu fallback) against BatchNorm2d(training) + LeakyReLU(0.2)
+    evaluated in float64 on the same bf16 input: y within bf16 rounding (2^-8 |ref| +
+    1e-3 rms), running statistics to 1e-5, and the backward -- with the activation mask
+    taken from the kernel's own y (sign(y) = sign(z)) -- gx within 2^-7 |ref| + 2e-3 rms,
+    gamma / beta gradients (fp32) within 1e-4 relative + 1e-4 rms.  The fallback (PyTorch's
+    bf16 BatchNorm output, then leaky_relu in bf16: two roundings) is checked 4x looser."""
+    from lie_vae import _lib
+    from lie_vae.experiments.nets import FusedBatchNormLeakyReLU
+    loose = 1.0 if _lib.load().lv_bn_supported(N * H * W, C) else 4.0
+    g = torch.Generator().manual_seed(N + C * 3 + H)
+    x = (torch.randn(N, C, H, W, generator=g) * 1.5 + 0.7).to(torch.bfloat16)
+    gy = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16)
+    m = FusedBatchNormLeakyReLU(C, 0.2).to(gpu_device)
+    with torch.no_grad():
+        m.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        m.bias.copy_(torch.randn(C, generator=g) * 0.3)
+        m.running_mean.copy_(torch.randn(C, generator=g) * 0.1)
+        m.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+    rm0, rv0 = m.running_mean.double().cpu(), m.running_var.double().cpu()
+    w64, b64 = m.weight.detach().double().cpu(), m.bias.detach().double().cpu()
+    xd = x.to(gpu_device).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = m(xd)
+    y.backward(gy.to(gpu_device).contiguous(memory_format=torch.channels_last))
+    assert y.dtype == torch.bfloat16 and int(m.num_batches_tracked) == 1
+    x64, g64 = x.double(), gy.double()
+    P = N * H * W
+    mean = x64.mean((0, 2, 3))
+    var = x64.var((0, 2, 3), unbiased=False)
+    inv = 1.0 / torch.sqrt(var + m.eps)
+    xhat = (x64 - mean.view(1, -1, 1, 1)) * inv.view(1, -1, 1, 1)
+    z = xhat * w64.view(1, -1, 1, 1) + b64.view(1, -1, 1, 1)
+    yref = torch.where(z > 0, z, 0.2 * z)
+    yd = y.detach().double().cpu()
+    rms = yref.square().mean().sqrt()
+    bad = (yd - yref).abs() > loose * (2.0 ** -8 * yref.abs() + 1e-3 * rms)
+    assert not bad.any(), f"y: {int(bad.sum())} off, max {(yd - yref).abs().max():.3e}"
+    torch.testing.assert_close(m.running_mean.double().cpu(), 0.9 * rm0 + 0.1 * mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m.running_var.double().cpu(), 0.9 * rv0 + 0.1 * var * P / (P - 1),
+                               rtol=1e-5, atol=1e-6)
+    gz = torch.where(yd > 0, g64, 0.2 * g64)
+    if loose > 1:  # the fallback's leaky_relu backward runs in bf16
+        gz = gz.to(torch.bfloat16).double()
+    gb = gz.sum((0, 2, 3))
+    gw = (gz * xhat).sum((0, 2, 3))
+    gx = (w64 * inv).view(1, -1, 1, 1) * (gz - gb.view(1, -1, 1, 1) / P - xhat * gw.view(1, -1, 1, 1) / P)
+    for name, got, ref, rel, absr in (("gx", xd.grad, gx, 2.0 ** -7, 2e-3), ("gw", m.weight.grad, gw, 1e-4, 1e-4),
+                                      ("gb", m.bias.grad, gb, 1e-4, 1e-4)):
+        gd = got.double().cpu()
+        rms = ref.square().mean().sqrt()
+        bad = (gd - ref).abs() > loose * (rel * ref.abs() + absr * rms)
+        assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max {(gd - ref).abs().max():.3e}"
