@@ -144,6 +144,7 @@ constexpr double kTileSegCostLarge = 560.0;  // ... many groups (>= kTileManyGro
 constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
+constexpr int kNumCUs = 256;                     // MI355X (persistent-grid A/B only)
 
 // A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
 // LV_*_NSEG force segment counts, LV_BWD_FGLOBAL forces the backward's global-spectrum
@@ -164,6 +165,7 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvTile = LV_KNOB("LV_TILE", 1);
   static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
   static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
+  static const int kEnvPersist = LV_KNOB("LV_TILE_PERSIST", 0);  // blocks per CU, 0 = off (A/B)
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
   const int Sw = 64 / a.C;
@@ -195,6 +197,13 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   p.lds = lds;
   p.gx = (int)groups;
   p.gy = nseg;
+  a.groups_loop = 0;
+  if (kEnvPersist > 0 && a.C == kTileFastC && nseg <= 8 && groups > (int64_t)kEnvPersist * kNumCUs) {
+    // persistent wave-specialised kernel: spectrum in its own LDS region, + 1 flush wave
+    a.groups_loop = groups;
+    p.gx = kEnvPersist * kNumCUs;
+    p.lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) + sizeof(float) * (2 * trig + (size_t)a.MC + 6 * Sw);
+  }
   return true;
 }
 

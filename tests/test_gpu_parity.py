@@ -408,6 +408,52 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     assert np.array_equal(outs[0]["gf"], outs[1]["gf"])
 
 
+_WS_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import lie_vae._ops as ops
+res = {}
+g = torch.Generator().manual_seed(21)
+for L, n, dt, with_mu in ((10, 5003, torch.float32, False), (10, 4001, torch.float32, True),
+                          (20, 3001, torch.bfloat16, False), (3, 3001, torch.float32, False)):
+    v = torch.randn(n, 3, generator=g).cuda().requires_grad_(True)
+    mu = torch.linalg.qr(torch.randn(n, 3, 3, generator=g))[0].cuda() if with_mu else None
+    F = torch.randn((L + 1) ** 2, 10, generator=g).cuda().requires_grad_(True)
+    y = ops.fused_exp_action(mu, v, F, L, out_dtype=dt)
+    tag = f"{L}_{n}_{with_mu}"
+    res["y" + tag] = y.float().detach().cpu().numpy()
+    if dt == torch.float32:
+        (y * torch.randn(y.shape, generator=g).cuda()).sum().backward()
+        res["gv" + tag] = v.grad.cpu().numpy()
+        res["gF" + tag] = F.grad.cpu().numpy()
+    ang = (torch.rand(n, 3, generator=g) * 6 - 3).cuda()
+    res["a" + tag] = ops.group_action(ang, F.detach(), L).cpu().numpy()
+np.savez(sys.argv[2], **res)
+"""
+
+
+def test_fwd_tile_persistent_wave_specialised_bitwise(gpu_device, tmp_path):
+    """The persistent wave-specialised forward tile kernel (action_fwd_tile_ws_kernel:
+    chain waves + a flush wave + a prologue wave over a grid that walks the sample groups;
+    A/B build, LV_TILE_PERSIST=1 -> 256 blocks) computes exactly the one-shot tile kernel's
+    arithmetic: fused outputs (fp32 with and without a mean rotation, bf16 at l = 20), the
+    angles the backward consumes (via bitwise gradients) and the plain group action."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "lie-vae_amd")
+    outs = []
+    for persist in ("0", "1"):
+        path = str(tmp_path / f"p{persist}.npz")
+        env = dict(os.environ, LV_TILE_PERSIST=persist,
+                   LIEVAE_HIP_LIB=os.path.join(pkg, "lie_vae", "liblievae_hip_ab.so"))
+        subprocess.run([sys.executable, "-c", _WS_SCRIPT, pkg, path], env=env, check=True, timeout=180)
+        outs.append(np.load(path))
+    assert sorted(outs[0].files) == sorted(outs[1].files)
+    for k in outs[0].files:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
 def test_exp_eazyz_vjp_matches_modular_bitwise(gpu_device):
     """lv_exp_eazyz_vjp (the fused path's prologue backward in one kernel) against the
     three modular kernels it replaces -- so3_exp_fwd / so3_sample_fwd, mat_to_eazyz_bwd,

@@ -302,7 +302,7 @@ __global__ __launch_bounds__(512) void c5_floor_kernel(ActionArgs a) {
 }
 template <int LT>
 __global__ __launch_bounds__(512) void c5_nomu_kernel(ActionArgs a) {
-  fwd_tile_body<LT, 10, true, __hip_bfloat16, false>(a);
+  fwd_tile_body<LT, 10, true, __hip_bfloat16, false>(a, blockIdx.x);
 }
 
 // the two-phase body without the 5-waves-per-SIMD register cap (105 VGPRs, no spills)

@@ -804,11 +804,11 @@ __global__ __launch_bounds__(512) void tile6_kernel(ActionArgs a) {
 template <int LT, int CT, bool MAYMU>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8)))
 void tile_w8_kernel(ActionArgs a) {
-  fwd_tile_body<LT, CT, true, float, MAYMU>(a);
+  fwd_tile_body<LT, CT, true, float, MAYMU>(a, blockIdx.x);
 }
 template <int LT, int CT>
 __global__ __launch_bounds__(512) void tile_nomu_kernel(ActionArgs a) {
-  fwd_tile_body<LT, CT, true, float, false>(a);
+  fwd_tile_body<LT, CT, true, float, false>(a, blockIdx.x);
 }
 
 }  // namespace lv
