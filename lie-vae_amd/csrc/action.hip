@@ -67,6 +67,39 @@ __global__ __launch_bounds__(64 * kBwdReduceWaves) void action_bwd_reduce_kernel
   }
 }
 
+// Variant (A/B build only until measured): one block per COLS consecutive elements, 1024
+// threads = 1024/COLS slab streams per element; stream k sums slabs k, k + S, k + 2S, ...
+// (all of a thread's loads issued together), then the S partials of an element are
+// added by a fixed-order halving tree in LDS.  Deterministic; a different (fixed)
+// summation order from action_bwd_reduce_kernel.
+template <int COLS>
+__global__ __launch_bounds__(1024) void action_bwd_reduce2_kernel(const float* ws_F, float* gF, int64_t MC,
+                                                                  int nslab) {
+  constexpr int S = 1024 / COLS;
+  __shared__ float part[S][COLS];
+  const int col = (int)threadIdx.x % COLS, k = (int)threadIdx.x / COLS;
+  const int64_t e = (int64_t)blockIdx.x * COLS + col;
+  float sum = 0.f;
+  if (e < MC) {
+    int b = k;
+    for (; b + 7 * S < nslab; b += 8 * S) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ws_F[(int64_t)(b + u * S) * MC + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; b < nslab; b += S) sum += ws_F[(int64_t)b * MC + e];
+  }
+  part[k][col] = sum;
+#pragma unroll
+  for (int h = S / 2; h >= 1; h >>= 1) {
+    __syncthreads();
+    if (k < h) part[k][col] += part[k + h][col];
+  }
+  if (k == 0 && e < MC) gF[e] = part[0][col];
+}
+
 namespace {
 
 template <int... Ls>
@@ -144,7 +177,6 @@ constexpr double kTileSegCostLarge = 560.0;  // ... many groups (>= kTileManyGro
 constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
-constexpr int kNumCUs = 256;                     // MI355X (persistent-grid A/B only)
 
 // A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
 // LV_*_NSEG force segment counts, LV_BWD_FGLOBAL forces the backward's global-spectrum
@@ -165,7 +197,6 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvTile = LV_KNOB("LV_TILE", 1);
   static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
   static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
-  static const int kEnvPersist = LV_KNOB("LV_TILE_PERSIST", 0);  // blocks per CU, 0 = off (A/B)
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
   const int Sw = 64 / a.C;
@@ -197,13 +228,6 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   p.lds = lds;
   p.gx = (int)groups;
   p.gy = nseg;
-  a.groups_loop = 0;
-  if (kEnvPersist > 0 && a.C == kTileFastC && nseg <= 8 && groups > (int64_t)kEnvPersist * kNumCUs) {
-    // persistent wave-specialised kernel: spectrum in its own LDS region, + 1 flush wave
-    a.groups_loop = groups;
-    p.gx = kEnvPersist * kNumCUs;
-    p.lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) + sizeof(float) * (2 * trig + (size_t)a.MC + 6 * Sw);
-  }
   return true;
 }
 
@@ -481,6 +505,20 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.stream = st;
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
+  static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", 0);  // A/B: 8 / 16 = reduce2 columns
+  if (kEnvReduce == 8) {
+    hipLaunchKernelGGL(action_bwd_reduce2_kernel<8>, dim3(ceil_div(MC, 8)), dim3(1024), 0, st,
+                       (const float*)workspace, gF, MC, b.gx);
+    LV_RETURN_LAUNCH("action_bwd_reduce2_kernel");
+  } else if (kEnvReduce == 16) {
+    hipLaunchKernelGGL(action_bwd_reduce2_kernel<16>, dim3(ceil_div(MC, 16)), dim3(1024), 0, st,
+                       (const float*)workspace, gF, MC, b.gx);
+    LV_RETURN_LAUNCH("action_bwd_reduce2_kernel");
+  } else if (kEnvReduce == 4) {
+    hipLaunchKernelGGL(action_bwd_reduce2_kernel<4>, dim3(ceil_div(MC, 4)), dim3(1024), 0, st,
+                       (const float*)workspace, gF, MC, b.gx);
+    LV_RETURN_LAUNCH("action_bwd_reduce2_kernel");
+  }
   hipLaunchKernelGGL(action_bwd_reduce_kernel, dim3(ceil_div(MC, kBwdReduceCols)), dim3(64 * kBwdReduceWaves),
                      0, st, (const float*)workspace, gF, MC, b.gx);
   LV_RETURN_LAUNCH("action_bwd_reduce_kernel");

@@ -25,10 +25,8 @@ struct ActionArgs {
   int64_t MC;
   int C, Sw, transpose;
   int fpitch;           // tile kernel: floats per wave-private spectrum slice in LDS
-  int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores, 2 = plain
+  int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores, 2 = plain (A/B)
   int seg_lo[kMaxSeg + 1];
-  int64_t groups_loop;  // tile kernel: 0 = one block per sample group, else the group count
-                        // a persistent grid walks (block b: groups b, b + gridDim.x, ...)
 };
 
 // ---- fused-prologue maths (per lane, registers).
@@ -206,7 +204,7 @@ __device__ __forceinline__ void lane_load(const ActionArgs& a, int64_t s, LaneIn
 template <bool FUSED, bool MAYMU = true>
 __device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& in, int64_t s,
                                             bool active, int c, bool write_ang, float c1[3],
-                                            float s1[3], float* ang_dst = nullptr) {
+                                            float s1[3]) {
   float cc[3], ss[3];
   if constexpr (FUSED) {
     float q[4];
@@ -218,10 +216,9 @@ __device__ __forceinline__ void lane_angles(const ActionArgs& a, const LaneIn& i
     if (write_ang && active && c == 0) {
       float ang[3];
       quat_to_eazyz_fwd(q, ang);
-      float* d = ang_dst ? ang_dst : a.ang_out + s * 3;  // ang_dst: an LDS slot (no global store)
-      d[0] = ang[0];
-      d[1] = ang[1];
-      d[2] = ang[2];
+      a.ang_out[s * 3 + 0] = ang[0];
+      a.ang_out[s * 3 + 1] = ang[1];
+      a.ang_out[s * 3 + 2] = ang[2];
     }
   } else {
 #pragma unroll

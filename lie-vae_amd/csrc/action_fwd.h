@@ -374,123 +374,6 @@ __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
   fwd_tile_body<LT, CT, FUSED, OutT>(a, blockIdx.x);
 }
 
-// Persistent, wave-specialised tile kernel (C = CT compile-time).  Per block: nseg chain
-// waves, one flush wave, one prologue wave; the grid walks the sample groups (g =
-// blockIdx.x, + gridDim.x, ...).  Per group g:
-//   chain waves:    chains of g (multiples buffer g & 1) into the LDS tile
-//   prologue wave:  angles + multiples of the next group into the other buffer, then the
-//                   loads of the group after that (in flight across the barriers)
-//                                                                          barrier A
-//   flush wave:     the tile out (ds_read_b128 -> 16-byte stores) + the group's angles
-//                                                                          barrier B
-// Only the flush wave stores and it never loads: on gfx9 vmcnt counts loads and stores in
-// one in-order queue, so a wave that stores and later loads waits for its stores (the
-// one-shot tile kernel sidesteps that by ending right after its flush).  The spectrum stays
-// in its own LDS region for the block's lifetime.
-template <int LT, int CT, bool FUSED, typename OutT>
-__global__ __launch_bounds__(640) __attribute__((amdgpu_waves_per_eu(LT <= 12 ? 6 : 5))) void action_fwd_tile_ws_kernel(ActionArgs a) {
-  static_assert(CT > 0, "compile-time C only");
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int kRow = TrigLds<LT>::kRow;
-  constexpr int C = CT, Sw = 64 / CT;
-  constexpr int MC = (LT + 1) * (LT + 1) * CT;
-  const int nseg = (int)(blockDim.x >> 6) - 2;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int stage_bytes = tile_stage_bytes(Sw, MC, (int)sizeof(OutT));
-  float* trig2 = lds + (stage_bytes >> 2);   // [2][Sw * kRow]
-  float* Fall = trig2 + 2 * Sw * kRow;       // (M, C) row-major
-  float* angs = Fall + MC;                   // [2][Sw * 3]
-  const int64_t ng = a.groups_loop;
-  const int64_t gstep = gridDim.x;
-  OutT* out = reinterpret_cast<OutT*>(a.out);
-  for (int e = (int)threadIdx.x; e < MC; e += (int)blockDim.x) Fall[e] = a.F[e];
-  int64_t g = blockIdx.x;
-  if (wave == nseg + 1) {
-    // ---------------------------------------------------------------- prologue wave
-    const bool task = lane < 3 * Sw;
-    const int jt = lane / 3, q = lane - 3 * (lane / 3);
-    const bool wang = FUSED && a.ang_out != nullptr;
-    auto sample = [&](int64_t grp) { return grp * Sw + min(jt, (int)min((int64_t)Sw, a.n - grp * Sw) - 1); };
-    LaneIn in;
-    auto prologue = [&](int64_t grp, int buf) {
-      const int Sv = (int)min((int64_t)Sw, a.n - grp * Sw);
-      float c1[3], s1[3];
-      lane_angles<FUSED>(a, in, sample(grp), jt < Sv, q, wang, c1, s1, angs + buf * Sw * 3 + jt * 3);
-      trig_row_fill<LT>(trig2 + buf * Sw * kRow + jt * kRow, c1, s1, q, LT);
-    };
-    if (task && g < ng) {
-      lane_load<FUSED>(a, sample(g), in);
-      prologue(g, 0);
-      if (g + gstep < ng) lane_load<FUSED>(a, sample(g + gstep), in);
-    }
-    block_sync_lds();
-    for (int k = 0; g < ng; g += gstep, ++k) {
-      if (task && g + gstep < ng) {
-        prologue(g + gstep, (k + 1) & 1);
-        if (g + 2 * gstep < ng) lane_load<FUSED>(a, sample(g + 2 * gstep), in);
-      }
-      block_sync_lds();  // A
-      block_sync_lds();  // B
-    }
-  } else if (wave == nseg) {
-    // ------------------------------------------------------------------ flush wave
-    block_sync_lds();
-    for (int k = 0; g < ng; g += gstep, ++k) {
-      block_sync_lds();  // A: the tile is complete
-      const int64_t s0 = g * Sw;
-      const int Sv = (int)min((int64_t)Sw, a.n - s0);
-      OutT* gout = out + s0 * MC;
-      const int mis = (int)(reinterpret_cast<uintptr_t>(gout) & 15);
-      const char* stage_b = reinterpret_cast<const char*>(lds) + mis;
-      const int nbytes = Sv * MC * (int)sizeof(OutT);
-      if (a.write_through == 1)
-        tile_flush<OutT, 16>(gout, stage_b, mis, nbytes, lane, 64);
-      else if (a.write_through == 2)
-        tile_flush<OutT, 0>(gout, stage_b, mis, nbytes, lane, 64);
-      else
-        tile_flush<OutT, 1>(gout, stage_b, mis, nbytes, lane, 64);
-      if (FUSED && a.ang_out != nullptr && lane < 3 * Sv) a.ang_out[s0 * 3 + lane] = angs[(k & 1) * Sw * 3 + lane];
-      block_sync_lds();  // B: the tile's reads have retired
-    }
-  } else {
-    // ------------------------------------------------------------------ chain waves
-    const int j = lane / C, c = lane - j * C;
-    const int lo = a.seg_lo[wave], hi = a.seg_lo[wave + 1];
-    block_sync_lds();
-    for (int k = 0; g < ng; g += gstep, ++k) {
-      const int64_t s0 = g * Sw;
-      const int Sv = (int)min((int64_t)Sw, a.n - s0);
-      const int mis = (int)(reinterpret_cast<uintptr_t>(out + s0 * MC) & 15);
-      OutT* st_lane = reinterpret_cast<OutT*>(reinterpret_cast<char*>(lds) + mis) + j * MC + c;
-      const float* tj = trig2 + (k & 1) * Sw * kRow + min(j, Sw - 1) * kRow;
-      const bool active = j < Sv;
-      sfor<LT + 1>([&](auto Lc) {
-        constexpr int l = LV_CV(Lc);
-        if (l >= lo && l < hi) {
-          constexpr int nn = 2 * l + 1;
-          constexpr int r0 = l * l;
-          float x[nn], y[nn];
-          sfor<nn>([&](auto K) { x[LV_CV(K)] = Fall[(r0 + LV_CV(K)) * C + c]; });
-          xrot_lds<l, 2, LT>(tj, x, y);
-          jmul<l>(y, x);
-          xrot_lds<l, 1, LT>(tj, x, y);
-          jmul<l>(y, x);
-          xrot_lds<l, 0, LT>(tj, x, y);
-          if (active) {
-            OutT* d = st_lane + r0 * C;
-            sfor<nn>([&](auto I) {
-              d[0] = tile_cvt(y[LV_CV(I)], (OutT*)nullptr);
-              d += C;
-            });
-          }
-        }
-      });
-      block_sync_lds();  // A
-      block_sync_lds();  // B
-    }
-  }
-}
 
 // ------------------------------------------------------------ Wigner-D blocks
 // Column q of D_l = chain applied to e_q; one thread per (sample, q), one kernel per
@@ -548,23 +431,6 @@ template <int LT>
 template <int CT>
 void FwdLauncher<LT>::launch_tile(FwdLaunch& p, bool bf16) {
   const dim3 grid(p.gx), block(64 * p.gy);
-  if constexpr (CT > 0) {
-    if (p.a.groups_loop > 0) {  // persistent wave-specialised variant (block = gy + 1 waves)
-      const dim3 wblock(64 * (p.gy + 2));
-      if (p.fused) {
-        if (bf16)
-          hipLaunchKernelGGL((action_fwd_tile_ws_kernel<LT, CT, true, __hip_bfloat16>), grid, wblock, p.lds, p.stream, p.a);
-        else
-          hipLaunchKernelGGL((action_fwd_tile_ws_kernel<LT, CT, true, float>), grid, wblock, p.lds, p.stream, p.a);
-      } else {
-        if (bf16)
-          hipLaunchKernelGGL((action_fwd_tile_ws_kernel<LT, CT, false, __hip_bfloat16>), grid, wblock, p.lds, p.stream, p.a);
-        else
-          hipLaunchKernelGGL((action_fwd_tile_ws_kernel<LT, CT, false, float>), grid, wblock, p.lds, p.stream, p.a);
-      }
-      return;
-    }
-  }
   if (p.fused) {
     if (bf16)
       hipLaunchKernelGGL((action_fwd_tile_kernel<LT, CT, true, __hip_bfloat16>), grid, block, p.lds, p.stream, p.a);

@@ -244,9 +244,14 @@ def test_action_bf16_output(gpu_device):
     ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n))
     spec = torch.randn((L + 1) ** 2, C, generator=gen)
     out = ops.group_action(ang.to(gpu_device), spec.to(gpu_device), L, out_dtype=torch.bfloat16)
-    ref = lie_ref.block_wigner_apply(ang[:256], spec.expand(256, -1, -1), L)
+    # every row, including the ragged last group (2048 = 341 * 6 + 2)
+    ref = lie_ref.block_wigner_apply(ang, spec.expand(n, -1, -1), L)
     assert out.dtype == torch.bfloat16
-    assert_normwise(host(out[:256].float()), ref.numpy(), 4e-3, what="bf16 out")
+    assert_normwise(host(out.float()), ref.numpy(), 4e-3, what="bf16 out")
+    y = host(out.float()).reshape(n, -1)
+    r = ref.numpy().reshape(n, -1)
+    err = np.linalg.norm(y - r, axis=1) / np.linalg.norm(r, axis=1)
+    assert err.max() <= 4e-3, f"bf16 out: worst row {err.argmax()} rel err {err.max():.2e}"
 
 
 # --------------------------------------------------------------- fused path
@@ -406,52 +411,6 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
         outs.append(np.load(path))
     assert np.array_equal(outs[0]["ga"], outs[1]["ga"])
     assert np.array_equal(outs[0]["gf"], outs[1]["gf"])
-
-
-_WS_SCRIPT = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-import lie_vae._ops as ops
-res = {}
-g = torch.Generator().manual_seed(21)
-for L, n, dt, with_mu in ((10, 5003, torch.float32, False), (10, 4001, torch.float32, True),
-                          (20, 3001, torch.bfloat16, False), (3, 3001, torch.float32, False)):
-    v = torch.randn(n, 3, generator=g).cuda().requires_grad_(True)
-    mu = torch.linalg.qr(torch.randn(n, 3, 3, generator=g))[0].cuda() if with_mu else None
-    F = torch.randn((L + 1) ** 2, 10, generator=g).cuda().requires_grad_(True)
-    y = ops.fused_exp_action(mu, v, F, L, out_dtype=dt)
-    tag = f"{L}_{n}_{with_mu}"
-    res["y" + tag] = y.float().detach().cpu().numpy()
-    if dt == torch.float32:
-        (y * torch.randn(y.shape, generator=g).cuda()).sum().backward()
-        res["gv" + tag] = v.grad.cpu().numpy()
-        res["gF" + tag] = F.grad.cpu().numpy()
-    ang = (torch.rand(n, 3, generator=g) * 6 - 3).cuda()
-    res["a" + tag] = ops.group_action(ang, F.detach(), L).cpu().numpy()
-np.savez(sys.argv[2], **res)
-"""
-
-
-def test_fwd_tile_persistent_wave_specialised_bitwise(gpu_device, tmp_path):
-    """The persistent wave-specialised forward tile kernel (action_fwd_tile_ws_kernel:
-    chain waves + a flush wave + a prologue wave over a grid that walks the sample groups;
-    A/B build, LV_TILE_PERSIST=1 -> 256 blocks) computes exactly the one-shot tile kernel's
-    arithmetic: fused outputs (fp32 with and without a mean rotation, bf16 at l = 20), the
-    angles the backward consumes (via bitwise gradients) and the plain group action."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    pkg = os.path.join(repo, "lie-vae_amd")
-    outs = []
-    for persist in ("0", "1"):
-        path = str(tmp_path / f"p{persist}.npz")
-        env = dict(os.environ, LV_TILE_PERSIST=persist,
-                   LIEVAE_HIP_LIB=os.path.join(pkg, "lie_vae", "liblievae_hip_ab.so"))
-        subprocess.run([sys.executable, "-c", _WS_SCRIPT, pkg, path], env=env, check=True, timeout=180)
-        outs.append(np.load(path))
-    assert sorted(outs[0].files) == sorted(outs[1].files)
-    for k in outs[0].files:
-        assert np.array_equal(outs[0][k], outs[1][k]), k
 
 
 def test_exp_eazyz_vjp_matches_modular_bitwise(gpu_device):

@@ -5,7 +5,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC EA requests).  Per
 MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of the bytes of wide (16 B/lane)
 coalesced streaming reads on gfx950 -- the kernel's reads (12 B/sample of v plus the
 4.8 KB spectrum per block) are narrow, so they are reported both raw and x2; WRITE_SIZE
-is exact for 16-B streaming stores (this kernel stores 8-B pairs, uncalibrated width).
+is exact for 16-B streaming stores (the tile kernel flushes with 16-B buffer stores).
 """
 import csv
 import glob
