@@ -70,6 +70,8 @@ def main():
                     help="stride-2 ConvTranspose2d: MIOpen's transposed convolution, one 3x3 "
                          "convolution + pixel shuffle (nets.PHASE_DECONV), or the library's MFMA "
                          "kernel for bf16 channels-last (nets.MFMA_DECONV)")
+    ap.add_argument("--fused-relu", choices=["on", "off"], default="on",
+                    help="DeconvNet's ReLUs inside the MFMA deconv kernels (nets.FUSED_RELU)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd, bwd, all-reduce, clip, Adam) in a "
                          "hipGraph and time its replays")
@@ -109,6 +111,7 @@ def main():
     nets.BIAS_GEMV = args.bias_grad == "gemv"
     nets.PHASE_DECONV = args.deconv == "phase"
     nets.MFMA_DECONV = args.deconv == "mfma"
+    nets.FUSED_RELU = args.fused_relu == "on"
 
     torch.manual_seed(0)
     model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,
@@ -158,7 +161,7 @@ def main():
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
                        "conv_gemm": args.conv_gemm, "bn": args.bn, "bias_grad": args.bias_grad,
-                       "deconv": args.deconv,
+                       "deconv": args.deconv, "fused_relu": args.fused_relu,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,

@@ -33,6 +33,20 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// ReLU of 8 packed bf16 (a 16-byte piece): max(bits, 0) as signed 16-bit integers zeroes
+// every value with the sign bit set (negatives, -0) and keeps the rest -- v_pk_max_i16.
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u32x4 relu_bf16x8(u32x4 v) {
+  const s16x8 t = __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), s16x8(0));
+  return __builtin_bit_cast(u32x4, t);
+}
+// g where x > 0 (ReLU backward against its output x), 8 packed bf16: x > 0 <=> the signed
+// 16-bit pattern is positive (a +NaN x also passes; the reference's mask would drop it).
+__device__ __forceinline__ u32x4 relu_mask_bf16x8(u32x4 g, u32x4 x) {
+  const s16x8 keep = __builtin_bit_cast(s16x8, x) > s16x8(0);  // lanes of -1 / 0
+  return g & __builtin_bit_cast(u32x4, keep);
+}
+
 constexpr int kBN = 208;               // output channels per tile (13 x 16; Cout <= kBN)
 constexpr int kNT = kBN / 16;          // 16-wide channel tiles
 constexpr int kBK = 32;                // K per step (one MFMA)
@@ -67,6 +81,9 @@ __global__ void deconv_pack_kernel(const __hip_bfloat16* w, __hip_bfloat16* wt, 
       v[e] = o < Cout ? w[((c0 + e) * Cout + o) * 16 + tap] : __float2bfloat16(0.f);
     *reinterpret_cast<u32x4*>(wt + ((int64_t)(p * kBN + o) * K + k0)) = *reinterpret_cast<const u32x4*>(v);
   }
+  // 64 zero bytes after the packed weight: the v2 kernel's source for taps outside the image
+  if (blockIdx.x == 0 && threadIdx.x < 4)
+    *reinterpret_cast<u32x4*>(wt + (int64_t)4 * kBN * K + 8 * threadIdx.x) = u32x4{0u, 0u, 0u, 0u};
 }
 
 struct DeconvArgs {
@@ -76,6 +93,7 @@ struct DeconvArgs {
   __hip_bfloat16* y;         // (N, 2H, 2W, Cout) bf16, channels-last
   int64_t M;                 // N*H*W pixels per phase
   int H, W, Cin, Cout;
+  int relu;                  // epilogue max(0, .) (the decoder's ReLU after the layer)
 };
 
 template <int BM>
@@ -202,9 +220,11 @@ __global__ __launch_bounds__(BM * 2) void deconv_mfma_kernel(DeconvArgs a) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            Cs[(wave * 32 - pass * SR + mt * 16 + cq + j) * kBN + o] =
-                __float2bfloat16(acc[mt][nt][j] + bo);
+          for (int j = 0; j < 4; ++j) {
+            float v = acc[mt][nt][j] + bo;
+            if (a.relu) v = fmaxf(v, 0.f);
+            Cs[(wave * 32 - pass * SR + mt * 16 + cq + j) * kBN + o] = __float2bfloat16(v);
+          }
       }
     }
     __syncthreads();
@@ -222,6 +242,183 @@ __global__ __launch_bounds__(BM * 2) void deconv_mfma_kernel(DeconvArgs a) {
   }
 }
 
+
+// v2 of the same GEMMs: the block's A (BM x 32) and B (kBN x 32) pieces go global -> LDS
+// by LDS-DMA (global_load_lds, 16 B per lane, no register staging) into an S-stage ring
+// issued S - 1 K-steps ahead, and the 8 waves tile the 256 x 208 block tile as 4 (rows) x 2
+// (channels): wave (wm, wn) owns 64 pixel rows x 7 | 6 channel tiles, so per K-step a wave
+// reads 4 A + 7 B fragments for 28 MFMAs (v1: 2 + 13 for 26).  The DMA writes 16 rows x
+// 64 B per wave instruction, so rows are unpadded and the 16-B k-chunks are XOR-swizzled
+// (chunk ^ (row >> 2) & 3): the 16 rows of a fragment read fall in 16 distinct 4-bank
+// groups.  Taps outside the image read 64 zero bytes kept after the packed weight.  Same
+// MFMA sequence per output element as v1: bitwise equal.
+constexpr int kV2BM = 256;
+constexpr int kV2NW = 7;                       // channel tiles per wave (wn = 1: 6)
+template <int S>
+struct DeconvV2 {
+  static constexpr int kA = kV2BM * kBK, kB = kBN * kBK;  // bf16 per stage
+  static constexpr size_t kLds = (size_t)S * (kA + kB) * 2;  // S = 2: 59,392 B, 3: 89,088 B
+};
+__device__ __forceinline__ int v2_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n wave-uniform
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+// XCD: 1-D grid whose consecutive block ids are dealt round-robin over the 8 XCDs; the four
+// phases of a pixel tile get ids b, b + 8, b + 16, b + 24, i.e. the same XCD at about the
+// same time, so the tile's input pixels come from HBM into that XCD's L2 once, not 4 times.
+template <int S, bool XCD>
+__global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
+  using T = DeconvV2<S>;
+  extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int p, tile;
+  if constexpr (XCD) {
+    const int bid = (int)blockIdx.x, slot = bid >> 3;
+    p = slot & 3;
+    tile = (bid & 7) + 8 * (slot >> 2);
+    if ((int64_t)tile * kV2BM >= a.M) return;  // grid padded to whole groups of 8 tiles
+  } else {
+    p = blockIdx.y;
+    tile = blockIdx.x;
+  }
+  const int r = p >> 1, s = p & 1;
+  const int64_t m0 = (int64_t)tile * kV2BM;
+  const int K = 4 * a.Cin;
+  const int nk = K / kBK;
+  const __hip_bfloat16* wtp = a.wt + (int64_t)p * kBN * K;
+  const __hip_bfloat16* zero16 = a.wt + (int64_t)4 * kBN * K;
+  const int lrow = lane >> 2, lslot = lane & 3;
+  // A DMA: rows 32 wave + 16 i + lrow (i = 0, 1)
+  int64_t abase[2];
+  int aa[2], ab[2], achunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 32 * wave + 16 * i + lrow;
+    achunk[i] = v2_swz(row, lslot);
+    const int64_t m = m0 + row;
+    if (m < a.M) {
+      const int64_t na = m / a.W;
+      ab[i] = (int)(m - na * a.W);
+      aa[i] = (int)(na % a.H);
+      abase[i] = (na / a.H) * a.H;
+    } else {
+      abase[i] = -1;
+      aa[i] = ab[i] = 0;
+    }
+  }
+  // B DMA: 16-row groups g = wave, wave + 8 (< kNT)
+  const int nbg = wave + 8 < kNT ? 2 : 1;
+  const int bchunk = v2_swz(lrow, lslot);  // (16 g + lrow) >> 2 & 3 == lrow >> 2 & 3
+  auto issue = [&](int ks, int stage) {
+    __hip_bfloat16* As = smem + stage * (T::kA + T::kB);
+    __hip_bfloat16* Bs = As + T::kA;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k0 = ks * kBK + achunk[i] * 8;
+      const int t = k0 / a.Cin, c = k0 - t * a.Cin;
+      const int ia = aa[i] + r - 1 + (t >> 1), ib = ab[i] + s - 1 + (t & 1);
+      const __hip_bfloat16* src = (abase[i] >= 0 && ia >= 0 && ia < a.H && ib >= 0 && ib < a.W)
+                                      ? a.x + ((abase[i] + ia) * a.W + ib) * a.Cin + c
+                                      : zero16;
+      __builtin_amdgcn_global_load_lds(src, as_lds(As + (32 * wave + 16 * i) * kBK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j < nbg) {
+        const int g = wave + 8 * j;
+        const __hip_bfloat16* src = wtp + (int64_t)(16 * g + lrow) * K + ks * kBK + bchunk * 8;
+        __builtin_amdgcn_global_load_lds(src, as_lds(Bs + 16 * g * kBK), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[4][kV2NW];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < kV2NW; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) issue(st, st);
+  const int per = 2 + nbg;  // DMA instructions per stage of this wave
+  const int fr = lane & 15, kc = lane >> 4;
+  const int ntw = wn == 0 ? kV2NW : kNT - kV2NW;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int stage = ks % S;
+    vm_wait(per * min(S - 2, nk - 1 - ks));  // this wave's pieces of step ks have landed
+    __syncthreads();                           // everyone's have; stage (ks - 1) % S is free
+    if (ks + S - 1 < nk) issue(ks + S - 1, (ks + S - 1) % S);
+    const __hip_bfloat16* As = smem + stage * (T::kA + T::kB);
+    const __hip_bfloat16* Bs = As + T::kA;
+    bf16x8 af[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int row = wm * 64 + mt * 16 + fr;
+      af[mt] = *reinterpret_cast<const bf16x8*>(As + row * kBK + v2_swz(row, kc) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < kV2NW; ++j) {
+      if (j < ntw) {
+        const int row = (wn * kV2NW + j) * 16 + fr;
+        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bs + row * kBK + v2_swz(row, kc) * 8);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bf, acc[mt][j], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: + bias (+ ReLU), bf16, staged [128 rows][kBN] in LDS per pass, 16-byte stores
+  __hip_bfloat16* Cs = smem;
+  const int cq = (lane >> 4) * 4;
+  const int pieces = a.Cout / 8;
+  const int H2 = 2 * a.H, W2 = 2 * a.W;
+  constexpr int SR = 128;
+#pragma unroll
+  for (int pass = 0; pass < kV2BM / SR; ++pass) {
+    __syncthreads();
+    if (wm * 64 / SR == pass) {
+#pragma unroll
+      for (int j = 0; j < kV2NW; ++j) {
+        if (j < ntw) {
+          const int o = (wn * kV2NW + j) * 16 + fr;
+          const float bo = (a.bias && o < a.Cout) ? a.bias[o] : 0.f;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float v = acc[mt][j][q] + bo;
+              if (a.relu) v = fmaxf(v, 0.f);
+              Cs[(wm * 64 - pass * SR + mt * 16 + cq + q) * kBN + o] = __float2bfloat16(v);
+            }
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < SR * pieces; e += 512) {
+      const int row = e / pieces, q = e - row * pieces;
+      const int64_t m = m0 + pass * SR + row;
+      if (m >= a.M) continue;
+      const int b = (int)(m % a.W);
+      const int64_t na = m / a.W;
+      const int aa_ = (int)(na % a.H);
+      const int64_t n = na / a.H;
+      __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 8;
+      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + row * kBN + q * 8);
+    }
+  }
+}
 
 // ----------------------------------------------------- small-Cout decoder layer
 // The decoder's last layer ConvTranspose2d(200, 3, 4, 2, 1) (nets.py:74): an N = 3
@@ -269,6 +466,7 @@ struct DeconvSmallArgs {
   const float* bias;          // (Cout) or null
   __hip_bfloat16* y;          // (N, 2H, 2W, Cout) bf16 channels-last
   int H, W, Cin, Cout, tiles_w;
+  int relu_in;                // the layer's input passes through ReLU first (x -> max(x, 0))
 };
 
 __global__ __launch_bounds__(kSmallThreads) void deconv_small_kernel(DeconvSmallArgs a) {
@@ -295,8 +493,10 @@ __global__ __launch_bounds__(kSmallThreads) void deconv_small_kernel(DeconvSmall
         const int px = pid >> 2, q = pid & 3;
         const int ia = a0 - 1 + px / kSiW, ib = b0 - 1 + px % kSiW;
         const int c = ch * 32 + q * 8;
-        if (ia >= 0 && ia < a.H && ib >= 0 && ib < a.W && c < a.Cin)
+        if (ia >= 0 && ia < a.H && ib >= 0 && ib < a.W && c < a.Cin) {
           rx[i] = *reinterpret_cast<const u32x4*>(ximg + ((int64_t)ia * a.W + ib) * a.Cin + c);
+          if (a.relu_in) rx[i] = relu_bf16x8(rx[i]);
+        }
       }
     }
 #pragma unroll
@@ -399,6 +599,8 @@ struct DeconvSmallBwdArgs {
   int H, W, Cin, Cout, nct, tiles_w;
   int tiles_img;              // tiles per image
   int64_t ntiles;
+  int relu_in;                // x is the input of a ReLU in front of the layer: the layer sees
+                              // max(x, 0) (wgrad) and gx is the gradient w.r.t. x (dgrad masks)
 };
 
 // wd[c][nbr·16 + n] = Wq[nbr, c, n] (0 past Cin, past 4·Cout and for nbr = 9): the dgrad
@@ -540,9 +742,12 @@ __global__ __launch_bounds__(kDgThreads) void deconv_small_dgrad_kernel(DeconvSm
     for (int e = tid; e < kBwPix * G8; e += kDgThreads) {
       const int px = e / G8, q = e - px * G8;
       const int ia = a0 + px / kBwTB, ib = b0 + px % kBwTB;
-      if (ia < a.H && ib < a.W)
-        *reinterpret_cast<u32x4*>(a.gx + ((n_img * a.H + ia) * a.W + ib) * a.Cin + 8 * q) =
-            *reinterpret_cast<const u32x4*>(os + px * pitch + 8 * q);
+      if (ia < a.H && ib < a.W) {
+        const int64_t off = ((n_img * a.H + ia) * a.W + ib) * a.Cin + 8 * q;
+        u32x4 v = *reinterpret_cast<const u32x4*>(os + px * pitch + 8 * q);
+        if (a.relu_in) v = relu_mask_bf16x8(v, *reinterpret_cast<const u32x4*>(a.x + off));
+        *reinterpret_cast<u32x4*>(a.gx + off) = v;
+      }
     }
   }
 }
@@ -594,8 +799,10 @@ __global__ __launch_bounds__(kWgThreads) void deconv_small_wgrad_kernel(DeconvSm
       const int ia = t.a0 + px / kBwTB, ib = t.b0 + px % kBwTB;
       xv[i] = u32x4{0u, 0u, 0u, 0u};
       if (e < kBwPix * G8 && ia < a.H && ib < a.W) {
-        if (c < a.Cin)
+        if (c < a.Cin) {
           xv[i] = *reinterpret_cast<const u32x4*>(a.x + ((t.n * a.H + ia) * a.W + ib) * a.Cin + c);
+          if (a.relu_in) xv[i] = relu_bf16x8(xv[i]);
+        }
         else if (c == a.Cin)
           xv[i][0] = 0x3f80u;  // bf16 1.0 in element 0 (channel Cin)
       }
@@ -754,9 +961,23 @@ __global__ __launch_bounds__(kCsThreads) void channel_sum_part_kernel(const __hi
 
 using namespace lv;
 
-constexpr int kDeconvAutoBM = 256;  // 1.6-2.1x MIOpen at batch 512 (profiles/r03_deconv_mfma.txt)
+// default forward variant: v2, 2-stage LDS-DMA ring, XCD-grouped phases (batch 512, 200 -> 200:
+// 36 / 72 / 282 us at H = 4 / 8 / 16 against v1's 43 / 88 / 344, bitwise equal;
+// profiles/r03_deconv_v2.txt)
+constexpr int kDeconvAutoBM = 4;
 
 namespace {
+template <int S, bool XCD>
+int launch_deconv_v2(const DeconvArgs& a, hipStream_t st) {
+  const int64_t tiles = (a.M + kV2BM - 1) / kV2BM;
+  if constexpr (XCD)
+    hipLaunchKernelGGL((deconv_mfma2_kernel<S, true>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
+                       DeconvV2<S>::kLds, st, a);
+  else
+    hipLaunchKernelGGL((deconv_mfma2_kernel<S, false>), dim3((unsigned)tiles, 4), dim3(512), DeconvV2<S>::kLds,
+                       st, a);
+  LV_RETURN_LAUNCH("deconv_mfma2_kernel");
+}
 template <int BM>
 int launch_deconv(const DeconvArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(deconv_mfma_kernel<BM>, dim3((unsigned)((a.M + BM - 1) / BM), 4),
@@ -769,7 +990,7 @@ extern "C" {
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                                int H, int W, int Cin, int Cout, int bm, void* stream);
 
-size_t lv_deconv4s2_packed_weight_elems(int Cin) { return 4 * (size_t)kBN * 4 * (size_t)Cin; }
+size_t lv_deconv4s2_packed_weight_elems(int Cin) { return 4 * (size_t)kBN * 4 * (size_t)Cin + 32; }
 
 int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, void* stream) {
   clear_error();
@@ -784,12 +1005,13 @@ int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, vo
 
 int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                           int H, int W, int Cin, int Cout, void* stream) {
-  return lv_deconv4s2_fwd_bf16_tile(x, wt, bias, y, N, H, W, Cin, Cout, 0, stream);
+  return lv_deconv4s2_fwd_bf16_ex(x, wt, bias, y, N, H, W, Cin, Cout, 0, stream);
 }
 
-int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
-                               int H, int W, int Cin, int Cout, int bm, void* stream) {
+static int deconv_fwd(const void* x, const void* wt, const float* bias, void* y, int64_t N, int H, int W,
+                      int Cin, int Cout, int bm, int flags, void* stream) {
   clear_error();
+  LV_CHECK_ARG((flags & ~LV_DECONV_RELU_OUT) == 0, "flags: only LV_DECONV_RELU_OUT for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
   LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 8 == 0, "Cout must be a multiple of 8 in [8, %d] (got %d)", kBN, Cout);
@@ -797,10 +1019,24 @@ int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias,
   LV_CHECK_ARG(x && wt && y, "null pointer");
   const int64_t M = N * H * W;
   LV_CHECK_ARG((M + 127) / 128 <= 0x7fffffff, "batch too large");
-  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256, "tile rows must be 0 (auto), 128 or 256");
-  DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout};
+  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256 || (bm >= 2 && bm <= 5),
+               "variant must be 0 (auto), 128 / 256 (v1 tile rows) or 2 / 3 (v2 stages), 4 / 5 (+ XCD order)");
+  DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout,
+               (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
   if (bm == 0) bm = kDeconvAutoBM;
+  if (bm == 2) return launch_deconv_v2<2, false>(a, (hipStream_t)stream);
+  if (bm == 3) return launch_deconv_v2<3, false>(a, (hipStream_t)stream);
+  if (bm == 4) return launch_deconv_v2<2, true>(a, (hipStream_t)stream);
+  if (bm == 5) return launch_deconv_v2<3, true>(a, (hipStream_t)stream);
   return bm == 256 ? launch_deconv<256>(a, (hipStream_t)stream) : launch_deconv<128>(a, (hipStream_t)stream);
+}
+int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
+                               int H, int W, int Cin, int Cout, int bm, void* stream) {
+  return deconv_fwd(x, wt, bias, y, N, H, W, Cin, Cout, bm, 0, stream);
+}
+int lv_deconv4s2_fwd_bf16_ex(const void* x, const void* wt, const float* bias, void* y, int64_t N,
+                             int H, int W, int Cin, int Cout, int flags, void* stream) {
+  return deconv_fwd(x, wt, bias, y, N, H, W, Cin, Cout, 0, flags, stream);
 }
 
 size_t lv_deconv4s2_small_packed_weight_elems(int Cin) { return (size_t)((Cin + 31) / 32) * 9 * 16 * 32; }
@@ -818,7 +1054,12 @@ int lv_deconv4s2_small_pack_weight_bf16(const void* w, void* wq, int Cin, int Co
 
 int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias, void* y, int64_t N,
                                 int H, int W, int Cin, int Cout, void* stream) {
+  return lv_deconv4s2_small_fwd_bf16_ex(x, wq, bias, y, N, H, W, Cin, Cout, 0, stream);
+}
+int lv_deconv4s2_small_fwd_bf16_ex(const void* x, const void* wq, const float* bias, void* y, int64_t N,
+                                   int H, int W, int Cin, int Cout, int flags, void* stream) {
   clear_error();
+  LV_CHECK_ARG((flags & ~LV_DECONV_RELU_IN) == 0, "flags: only LV_DECONV_RELU_IN for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
   LV_CHECK_ARG(Cout >= 1 && Cout <= kSmallMaxCout, "Cout must be in [1, %d] (got %d)", kSmallMaxCout, Cout);
@@ -826,7 +1067,8 @@ int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias
   if (N == 0) return LV_OK;
   LV_CHECK_ARG(x && wq && y, "null pointer");
   const int th = (H + kSqH - 1) / kSqH, tw = (W + kSqW - 1) / kSqW;
-  DeconvSmallArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wq, bias, (__hip_bfloat16*)y, H, W, Cin, Cout, tw};
+  DeconvSmallArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wq, bias, (__hip_bfloat16*)y, H, W, Cin, Cout, tw,
+                    (flags & LV_DECONV_RELU_IN) ? 1 : 0};
   hipLaunchKernelGGL(deconv_small_kernel, dim3(th * tw, (unsigned)N), dim3(kSmallThreads), 0,
                      (hipStream_t)stream, a);
   LV_RETURN_LAUNCH("deconv_small_kernel");
@@ -875,7 +1117,13 @@ size_t lv_deconv4s2_small_bwd_workspace_elems(int64_t N, int H, int W, int Cin, 
 
 int lv_deconv4s2_small_bwd_bf16(const void* x, const void* gy, const void* wd, void* gx, void* gw, float* gb,
                                 float* ws, int64_t N, int H, int W, int Cin, int Cout, void* stream) {
+  return lv_deconv4s2_small_bwd_bf16_ex(x, gy, wd, gx, gw, gb, ws, N, H, W, Cin, Cout, 0, stream);
+}
+int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd, void* gx, void* gw, float* gb,
+                                   float* ws, int64_t N, int H, int W, int Cin, int Cout, int flags,
+                                   void* stream) {
   clear_error();
+  LV_CHECK_ARG((flags & ~LV_DECONV_RELU_IN) == 0, "flags: only LV_DECONV_RELU_IN for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0 && small_bwd_nct(Cin) <= kBwMaxCt,
                "Cin must be a positive multiple of 8 below %d (got %d)", 16 * kBwMaxCt, Cin);
@@ -887,7 +1135,8 @@ int lv_deconv4s2_small_bwd_bf16(const void* x, const void* gy, const void* wd, v
   const int tw = (W + kBwTB - 1) / kBwTB, th = (H + kBwTA - 1) / kBwTA;
   const int64_t ntiles = N * th * tw;
   DeconvSmallBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)gy, (const __hip_bfloat16*)wd,
-                       (__hip_bfloat16*)gx, ws, H, W, Cin, Cout, small_bwd_nct(Cin), tw, th * tw, ntiles};
+                       (__hip_bfloat16*)gx, ws, H, W, Cin, Cout, small_bwd_nct(Cin), tw, th * tw, ntiles,
+                       (flags & LV_DECONV_RELU_IN) ? 1 : 0};
   const int nw = Cin * Cout * 16;
   if (ntiles == 0) {  // empty batch: zero gradients
     if (gw) LV_CHECK_HIP(hipMemsetAsync(gw, 0, (size_t)nw * 2, st));

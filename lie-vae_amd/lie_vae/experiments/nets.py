@@ -247,6 +247,10 @@ PHASE_DECONV = False  # off: 10.5 vs 7.4 ms (bf16), 22.1 vs 15.2 ms (f32)
 # in bf16 (autocast) on channels-last inputs; fp32 / NCHW / unsupported shapes keep MIOpen.
 # Config 3 bf16: 7.41 -> 6.29 ms/step (dec5 forward 989 -> 77 us, dec2-4 2x faster).
 MFMA_DECONV = True
+# DeconvNet's ReLUs fused into the neighbouring MFMA layers (MfmaConvTranspose2d.relu_out /
+# relu_in): the forward clamps and the largest ReLU backward (after the 4th layer, folded
+# into the RGB layer's dgrad epilogue) leave the step.
+FUSED_RELU = True
 
 
 def _channel_sum(g):
@@ -267,15 +271,24 @@ class _Deconv4s2(torch.autograd.Function):
     kernels (x, w bf16; b fp32 added before the bf16 rounding).  Backward: for Cout <= 4
     the library's quad-view dgrad / wgrad / bias kernels (lv_deconv4s2_small_bwd_bf16);
     otherwise aten.convolution_backward on the saved bf16 operands (what MIOpen computes
-    for the plain layer) for gx, gw and the library's per-channel sum for gb."""
+    for the plain layer) for gx, gw and the library's per-channel sum for gb.
+
+    flags (include/lievae.h): LV_DECONV_RELU_OUT (Cout > 4) returns relu(y) from the
+    forward epilogue, and the backward masks gy by y > 0 (ReLU's backward against its
+    output) before the layer's own; LV_DECONV_RELU_IN (Cout <= 4) makes the layer read
+    relu(x): forward and wgrad stage max(x, 0), and dgrad's epilogue masks gx by x > 0, so
+    the returned gx is the gradient w.r.t. the ReLU's input.  Both reproduce the unfused
+    nn.ReLU + layer bit for bit."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, flags=0):
         from .. import _lib
         N, Cin, H, W = x.shape
         Cout = w.shape[1]
         wc = w.contiguous()
         small = Cout <= 4  # the RGB output layer: quad GEMM over the 3x3 neighbourhood
+        ok = _lib.LV_DECONV_RELU_IN if small else _lib.LV_DECONV_RELU_OUT
+        assert flags & ~ok == 0, f"flags {flags} not supported for Cout={Cout}"
         pre = "lv_deconv4s2_small_" if small else "lv_deconv4s2_"
         wt = torch.empty(getattr(_lib.load(), pre + "packed_weight_elems")(Cin), device=x.device,
                          dtype=torch.bfloat16)
@@ -283,20 +296,24 @@ class _Deconv4s2(torch.autograd.Function):
                         memory_format=torch.channels_last)
         st = _lib.stream()
         _lib.call(pre + "pack_weight_bf16", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
-        _lib.call(pre + "fwd_bf16", x.data_ptr(), wt.data_ptr(),
-                  None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, st)
-        ctx.save_for_backward(x, wc)
+        _lib.call(pre + "fwd_bf16_ex", x.data_ptr(), wt.data_ptr(),
+                  None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, flags, st)
+        relu_out = bool(flags & _lib.LV_DECONV_RELU_OUT)
+        ctx.save_for_backward(x, wc, *((y,) if relu_out else ()))
         ctx.has_bias = b is not None
+        ctx.flags = flags
         return y
 
     @staticmethod
     def backward(ctx, gy):
         from .. import _lib
-        x, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors[:2]
         N, Cin, H, W = x.shape
         Cout = w.shape[1]
         gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        need_x, need_w, need_b = ctx.needs_input_grad
+        if ctx.flags & _lib.LV_DECONV_RELU_OUT:
+            gy = torch.ops.aten.threshold_backward(gy, ctx.saved_tensors[2], 0)
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
         need_b = need_b and ctx.has_bias
         if Cout <= 4:
             lib, st = _lib.load(), _lib.stream()
@@ -312,19 +329,31 @@ class _Deconv4s2(torch.autograd.Function):
                 gb = torch.empty(Cout, device=x.device, dtype=torch.float32) if need_b else None
                 ws = torch.empty(max(1, lib.lv_deconv4s2_small_bwd_workspace_elems(N, H, W, Cin, Cout)),
                                  device=x.device, dtype=torch.float32)
-            _lib.call("lv_deconv4s2_small_bwd_bf16", x.data_ptr(), gy.data_ptr(),
+            _lib.call("lv_deconv4s2_small_bwd_bf16_ex", x.data_ptr(), gy.data_ptr(),
                       None if wd is None else wd.data_ptr(), None if gx is None else gx.data_ptr(),
                       None if gw is None else gw.data_ptr(), None if gb is None else gb.data_ptr(),
-                      None if ws is None else ws.data_ptr(), N, H, W, Cin, Cout, st)
-            return gx, (gw if need_w else None), gb
+                      None if ws is None else ws.data_ptr(), N, H, W, Cin, Cout, ctx.flags, st)
+            return gx, (gw if need_w else None), gb, None
         gx, gw, _ = torch.ops.aten.convolution_backward(
             gy, x, w, None, [2, 2], [1, 1], [1, 1], True, [0, 0], 1, [need_x, need_w, False])
-        return gx, gw, (_channel_sum(gy) if need_b else None)
+        return gx, gw, (_channel_sum(gy) if need_b else None), None
 
 
 class MfmaConvTranspose2d(nn.ConvTranspose2d):
     """nn.ConvTranspose2d (same parameters / state_dict) whose k4 s2 p1 forward runs on
-    the MFMA kernel for bf16 channels-last inputs (autocast bf16, or bf16 tensors)."""
+    the MFMA kernel for bf16 channels-last inputs (autocast bf16, or bf16 tensors).
+
+    relu_in / relu_out (plain attributes, not state): the layer computes
+    layer(relu(x)) / relu(layer(x)) -- DeconvNet moves its nn.ReLU modules into the
+    neighbouring layers this way (FUSED_RELU); the MFMA path fuses relu_out for Cout > 4
+    and relu_in for Cout <= 4 into the kernels, everything else applies F.relu."""
+
+    relu_in = False
+    relu_out = False
+
+    def extra_repr(self):
+        fl = [n for n in ("relu_in", "relu_out") if getattr(self, n)]
+        return super().extra_repr() + "".join(f", {n}=True" for n in fl)
 
     def _mfma_ok(self, x):
         return (x.is_cuda and x.dim() == 4 and _cl(x) and self.kernel_size == (4, 4)
@@ -335,14 +364,23 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
                      or self.out_channels <= 4) and x.shape[0] <= 65535)
 
     def forward(self, x, output_size=None):
+        F_ = torch.nn.functional
         bf16 = x.dtype == torch.bfloat16 or (
             torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
         if output_size is not None or not bf16 or not self._mfma_ok(x):
-            return super().forward(x, output_size)
+            y = super().forward(F_.relu(x) if self.relu_in else x, output_size)
+            return F_.relu(y) if self.relu_out else y
+        from .. import _lib
+        small = self.out_channels <= 4
+        flags = ((_lib.LV_DECONV_RELU_IN if self.relu_in and small else 0)
+                 | (_lib.LV_DECONV_RELU_OUT if self.relu_out and not small else 0))
         with torch.autocast("cuda", enabled=False):
             xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            return _Deconv4s2.apply(xb, self.weight.to(torch.bfloat16),
-                                    None if self.bias is None else self.bias.float())
+            if self.relu_in and not small:
+                xb = F_.relu(xb)
+            y = _Deconv4s2.apply(xb, self.weight.to(torch.bfloat16),
+                                 None if self.bias is None else self.bias.float(), flags)
+            return F_.relu(y) if self.relu_out and small else y
 
 
 class PhaseConvTranspose2d(nn.ConvTranspose2d):
@@ -451,13 +489,22 @@ class ConvNetBN(nn.Sequential):
 
 
 class DeconvNet(nn.Sequential):
-    """1x1 -> 64x64 transposed-conv stack — nets.py:60-75."""
+    """1x1 -> 64x64 transposed-conv stack — nets.py:60-75.  With FUSED_RELU (and the MFMA
+    layers) the ReLUs after the 2nd and 3rd layers become the layers' relu_out and the
+    ReLU after the 4th becomes the RGB layer's relu_in (the kernels apply them); their
+    slots hold nn.Identity, so module indices and state_dict keys are the reference's."""
 
     def __init__(self, in_dims, hidden_dims, rgb=False):
         layers = [View(-1, in_dims, 1, 1), _convt(in_dims, hidden_dims, 4, 1, 0), nn.ReLU()]
         for _ in range(3):
             layers += [_convt_s2(hidden_dims, hidden_dims, 4, 2, 1), nn.ReLU()]
         layers.append(_convt_s2(hidden_dims, 3 if rgb else 1, 4, 2, 1))
+        if FUSED_RELU and MFMA_DECONV:
+            for i in (3, 5):  # layers 2, 3: relu_out
+                layers[i].relu_out = True
+                layers[i + 1] = nn.Identity()
+            layers[9].relu_in = True  # the RGB layer reads relu(layer 4's output)
+            layers[8] = nn.Identity()
         super().__init__(*layers)
 
 

@@ -596,6 +596,40 @@ def test_mfma_deconv_backward_matches_autograd(gpu_device, N, Cin, Cout, H, W):
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
 
 
+def test_fused_relu_deconvnet_bitwise(gpu_device, monkeypatch):
+    """DeconvNet with its ReLUs fused into the MFMA layers (nets.FUSED_RELU: relu_out on the
+    2nd / 3rd layers' forward epilogue, relu_in on the RGB layer -- max(x, 0) staged by its
+    forward and wgrad, gx masked by x > 0 in its dgrad epilogue) against the same network
+    with plain nn.ReLU modules, bf16 autocast, channels-last: output and every parameter
+    and input gradient bit for bit (ReLU commutes with the bf16 rounding; the masks are the
+    same comparisons).  MIOpen (the 200 -> 200 layers' backward) is pinned to deterministic
+    solutions: its default weight-gradient kernels may accumulate in any order."""
+    from lie_vae.experiments import nets
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
+    torch.manual_seed(5)
+    mods = []
+    for fused in (True, False):
+        monkeypatch.setattr(nets, "FUSED_RELU", fused)
+        mods.append(nets.DeconvNet(1210, 200, rgb=True).to(gpu_device).to(memory_format=torch.channels_last))
+    mods[1].load_state_dict(mods[0].state_dict())
+    assert isinstance(mods[0][8], torch.nn.Identity) and mods[0][9].relu_in
+    assert isinstance(mods[1][8], torch.nn.ReLU)
+    z = torch.randn(6, 1210, device=gpu_device)
+    gy = torch.randn(6, 3, 64, 64, device=gpu_device)
+    outs = []
+    for m in mods:
+        zi = z.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(zi)
+        (y.float() * gy).sum().backward()
+        outs.append((y.detach(), zi.grad, [p.grad for p in m.parameters()]))
+    assert torch.equal(outs[0][0], outs[1][0]), "forward"
+    assert torch.equal(outs[0][1], outs[1][1]), "input gradient"
+    for i, (a, b) in enumerate(zip(outs[0][2], outs[1][2])):
+        assert torch.equal(a, b), f"parameter {i} gradient"
+
+
 @pytest.mark.parametrize("N,C,H,W", [(64, 50, 32, 32), (16, 100, 16, 16), (32, 200, 8, 8), (64, 400, 4, 4),
                                      (3, 24, 5, 7), (2, 12, 3, 3), (2, 6, 4, 4)])
 def test_fused_bn_leaky_relu_matches_float64(gpu_device, N, C, H, W):

@@ -1,6 +1,7 @@
 """Decoder ConvTranspose2d(200, 200, 4, 2, 1) forward at the config-3 batch (512), bf16
-NHWC: MIOpen (torch conv_transpose2d) vs the library's MFMA kernel (lv_deconv4s2_fwd_bf16,
-pack + GEMM), HIP events over 50 calls each.  FLOPs = 2 * N * Cin * Cout * 16 * H * W."""
+NHWC: MIOpen (torch conv_transpose2d) vs the library's MFMA kernels (lv_deconv4s2_fwd_bf16,
+pack + GEMM; v1 at 128 / 256 pixel rows, v2 with a 2 / 3-stage LDS-DMA ring), HIP events
+over 50 calls each, v2 output bit-compared with v1.  FLOPs = 2 * N * Cin * Cout * 16 * H * W."""
 import json
 import sys
 import torch
@@ -31,7 +32,9 @@ for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16), (512, 3, 32)]:
     runs = [("miopen", lambda: torch.nn.functional.conv_transpose2d(x, wcl, b.to(torch.bfloat16), 2, 1)),
             ("mfma", lambda: _Deconv4s2.apply(x, w, b))]
     if big:
-        runs += [("gemm_bm128", lambda: kern(128)), ("gemm_bm256", lambda: kern(256))]
+        runs += [("gemm_bm128", lambda: kern(128)), ("gemm_bm256", lambda: kern(256)),
+                 ("v2_s2", lambda: kern(2)), ("v2_s3", lambda: kern(3)),
+                 ("v2_s2_xcd", lambda: kern(4)), ("v2_s3_xcd", lambda: kern(5)), ("gemm_bm256b", lambda: kern(256))]
     for tag, fn in runs:
         for _ in range(5):
             fn()
@@ -45,6 +48,13 @@ for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16), (512, 3, 32)]:
         us = e0.elapsed_time(e1) * 1e3 / 50
         row[tag + "_us"] = us
         row[tag + "_TFLOPs"] = flops / us / 1e6
+    if big:  # v2 (both ring depths) against v1: the same MFMA sequence per element
+        kern(256)
+        y1 = yk.clone()
+        for v in (2, 3, 4, 5):
+            yk.fill_(float("nan"))
+            kern(v)
+            row[f"v2_{v}_bitwise_vs_v1"] = bool(torch.equal(yk, y1))
     ref = torch.nn.functional.conv_transpose2d(x.float(), w.float(), b, 2, 1)
     y = _Deconv4s2.apply(x, w, b).float()
     row["max_rel_err_vs_f32"] = float(((y - ref).abs().max() / ref.abs().max()).item())
