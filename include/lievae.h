@@ -250,9 +250,13 @@ int lv_bn_lrelu_bwd_bf16(const void* g, const void* x, const float* gamma, const
  *   LV_DECONV_RELU_OUT  y = max(conv_transpose(x) + b, 0) (the ReLU after the layer);
  *   LV_DECONV_RELU_IN   the layer reads max(x, 0) (the ReLU in front of it): forward and
  *                       wgrad use max(x, 0) and gx is the gradient w.r.t. x itself (masked
- *                       by x > 0).  Small-Cout layer only. */
+ *                       by x > 0).  Small-Cout layer only;
+ *   LV_DECONV_MASK_GX   (backward, small-Cout layer) gx masked by x > 0 only: x is already a
+ *                       ReLU output (e.g. written with LV_DECONV_RELU_OUT), so forward and
+ *                       wgrad need no max and gx is the gradient w.r.t. the ReLU's input. */
 #define LV_DECONV_RELU_OUT 1
 #define LV_DECONV_RELU_IN 2
+#define LV_DECONV_MASK_GX 4
 int lv_deconv4s2_fwd_bf16_ex(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                              int H, int W, int Cin, int Cout, int flags, void* stream);
 int lv_deconv4s2_small_fwd_bf16_ex(const void* x, const void* wq, const float* bias, void* y,

@@ -600,7 +600,7 @@ struct DeconvSmallBwdArgs {
   int tiles_img;              // tiles per image
   int64_t ntiles;
   int relu_in;                // x is the input of a ReLU in front of the layer: the layer sees
-                              // max(x, 0) (wgrad) and gx is the gradient w.r.t. x (dgrad masks)
+                              // max(x, 0) (wgrad); dgrad masks gx by x > 0 (template MASK)
 };
 
 // wd[c][nbr·16 + n] = Wq[nbr, c, n] (0 past Cin, past 4·Cout and for nbr = 9): the dgrad
@@ -671,7 +671,10 @@ __device__ __forceinline__ TileAt tile_at(const DeconvSmallBwdArgs& a, int64_t t
 // 16-byte quad reads (B operand: K = 8 consecutive (nbr, n) of one pixel), five MFMAs per
 // channel tile (C rows = 4 consecutive channels per lane -> one 8-byte LDS store), then the
 // staged [64 pixels][Cin] tile leaves as 16-byte stores of whole pixel rows.
-template <int CO>
+// MASK: gx is masked by x > 0 (the ReLU in front of the layer, LV_DECONV_RELU_IN /
+// LV_DECONV_MASK_GX); the tile's x pieces are loaded right after the quad stage, so their
+// latency hides under the tile's MFMAs.
+template <int CO, bool MASK>
 __global__ __launch_bounds__(kDgThreads) void deconv_small_dgrad_kernel(DeconvSmallBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 sm[];
   __hip_bfloat16* qs = sm;                               // [kBwQuads + 1][16], last = zeros
@@ -707,11 +710,24 @@ __global__ __launch_bounds__(kDgThreads) void deconv_small_dgrad_kernel(DeconvSm
   TileAt at = tile_at(a, tile);
   if (tile < a.ntiles) qst.load(a, at.n, at.a0, at.b0, tid);
   __syncthreads();  // the zeroed quad image
+  constexpr int kXm = MASK ? (kBwPix * kBwMaxCt * 2 + kDgThreads - 1) / kDgThreads : 1;  // 8
+  u32x4 xm[kXm];
   for (; tile < a.ntiles; tile += gridDim.x) {
     const int64_t n_img = at.n;
     const int a0 = at.a0, b0 = at.b0;
     qst.store(qs, tid);
     __syncthreads();
+    if constexpr (MASK) {  // this tile's x pieces, in the store loop's order
+#pragma unroll
+      for (int i = 0; i < kXm; ++i) {
+        const int e = tid + i * kDgThreads;
+        const int px = e / G8, q = e - px * G8;
+        const int ia = a0 + px / kBwTB, ib = b0 + px % kBwTB;
+        xm[i] = u32x4{0u, 0u, 0u, 0u};
+        if (e < kBwPix * G8 && ia < a.H && ib < a.W)
+          xm[i] = *reinterpret_cast<const u32x4*>(a.x + ((n_img * a.H + ia) * a.W + ib) * a.Cin + 8 * q);
+      }
+    }
     if (tile + gridDim.x < a.ntiles) {  // next tile's quads in flight during this tile's MFMAs
       at = tile_at(a, tile + gridDim.x);
       qst.load(a, at.n, at.a0, at.b0, tid);
@@ -739,14 +755,26 @@ __global__ __launch_bounds__(kDgThreads) void deconv_small_dgrad_kernel(DeconvSm
       }
     }
     __syncthreads();
-    for (int e = tid; e < kBwPix * G8; e += kDgThreads) {
+#pragma unroll
+    for (int i = 0; i < kXm; ++i) {
+      const int e = tid + i * kDgThreads;
+      if (e >= kBwPix * G8) break;
       const int px = e / G8, q = e - px * G8;
       const int ia = a0 + px / kBwTB, ib = b0 + px % kBwTB;
       if (ia < a.H && ib < a.W) {
         const int64_t off = ((n_img * a.H + ia) * a.W + ib) * a.Cin + 8 * q;
         u32x4 v = *reinterpret_cast<const u32x4*>(os + px * pitch + 8 * q);
-        if (a.relu_in) v = relu_mask_bf16x8(v, *reinterpret_cast<const u32x4*>(a.x + off));
+        if constexpr (MASK) v = relu_mask_bf16x8(v, xm[i]);
         *reinterpret_cast<u32x4*>(a.gx + off) = v;
+      }
+    }
+    if constexpr (!MASK) {  // kXm = 1 covers only the first pass: the rest of the tile
+      for (int e = tid + kDgThreads; e < kBwPix * G8; e += kDgThreads) {
+        const int px = e / G8, q = e - px * G8;
+        const int ia = a0 + px / kBwTB, ib = b0 + px % kBwTB;
+        if (ia < a.H && ib < a.W)
+          *reinterpret_cast<u32x4*>(a.gx + ((n_img * a.H + ia) * a.W + ib) * a.Cin + 8 * q) =
+              *reinterpret_cast<const u32x4*>(os + px * pitch + 8 * q);
       }
     }
   }
@@ -1123,7 +1151,8 @@ int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd
                                    float* ws, int64_t N, int H, int W, int Cin, int Cout, int flags,
                                    void* stream) {
   clear_error();
-  LV_CHECK_ARG((flags & ~LV_DECONV_RELU_IN) == 0, "flags: only LV_DECONV_RELU_IN for this layer");
+  LV_CHECK_ARG((flags & ~(LV_DECONV_RELU_IN | LV_DECONV_MASK_GX)) == 0,
+               "flags: only LV_DECONV_RELU_IN / LV_DECONV_MASK_GX for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0 && small_bwd_nct(Cin) <= kBwMaxCt,
                "Cin must be a positive multiple of 8 below %d (got %d)", 16 * kBwMaxCt, Cin);
@@ -1145,8 +1174,11 @@ int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd
   }
   if (gx) {
     const size_t lds = ((size_t)(kBwQuads + 1) * 16 + (size_t)kBwPix * (a.nct * 16 + 8)) * 2;
-    auto k = Cout == 1 ? deconv_small_dgrad_kernel<1> : Cout == 2 ? deconv_small_dgrad_kernel<2>
-           : Cout == 3 ? deconv_small_dgrad_kernel<3> : deconv_small_dgrad_kernel<4>;
+    const bool mask = (flags & (LV_DECONV_RELU_IN | LV_DECONV_MASK_GX)) != 0;
+    auto k = mask ? (Cout == 1 ? deconv_small_dgrad_kernel<1, true> : Cout == 2 ? deconv_small_dgrad_kernel<2, true>
+                     : Cout == 3 ? deconv_small_dgrad_kernel<3, true> : deconv_small_dgrad_kernel<4, true>)
+                  : (Cout == 1 ? deconv_small_dgrad_kernel<1, false> : Cout == 2 ? deconv_small_dgrad_kernel<2, false>
+                     : Cout == 3 ? deconv_small_dgrad_kernel<3, false> : deconv_small_dgrad_kernel<4, false>);
     const int blocks = (int)std::min<int64_t>(ntiles, resident_blocks((const void*)k, kDgThreads, lds));
     hipLaunchKernelGGL(k, dim3(blocks), dim3(kDgThreads), lds, st, a);
     LV_CHECK_LAUNCH("deconv_small_dgrad_kernel");

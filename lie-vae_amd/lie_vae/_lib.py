@@ -75,7 +75,7 @@ _SIGS["lv_deconv4s2_small_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I
 _SIGS["lv_deconv4s2_fwd_bf16_ex"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_fwd_bf16_ex"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_bwd_bf16_ex"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
-LV_DECONV_RELU_OUT, LV_DECONV_RELU_IN = 1, 2  # include/lievae.h
+LV_DECONV_RELU_OUT, LV_DECONV_RELU_IN, LV_DECONV_MASK_GX = 1, 2, 4  # include/lievae.h
 _SIGS["lv_channel_sum_bf16"] = [_P, _P, _P, _I64, _I, _P]
 _SIGS["lv_bn_lrelu_fwd_bf16"] = [_P, _P, _P, _P, _P, _I, _F, _F, _F, _P, _P, _P, _P, _I64, _I, _P]
 _SIGS["lv_bn_lrelu_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I64, _I, _P]

@@ -275,10 +275,14 @@ class _Deconv4s2(torch.autograd.Function):
 
     flags (include/lievae.h): LV_DECONV_RELU_OUT (Cout > 4) returns relu(y) from the
     forward epilogue, and the backward masks gy by y > 0 (ReLU's backward against its
-    output) before the layer's own; LV_DECONV_RELU_IN (Cout <= 4) makes the layer read
-    relu(x): forward and wgrad stage max(x, 0), and dgrad's epilogue masks gx by x > 0, so
-    the returned gx is the gradient w.r.t. the ReLU's input.  Both reproduce the unfused
-    nn.ReLU + layer bit for bit."""
+    output) before the layer's own -- unless SKIP_MASK says the consumer of y already
+    returns a masked gradient; LV_DECONV_RELU_IN (Cout <= 4) makes the layer read relu(x):
+    forward and wgrad stage max(x, 0), and dgrad's epilogue masks gx by x > 0, so the
+    returned gx is the gradient w.r.t. the ReLU's input; LV_DECONV_MASK_GX (Cout <= 4) is
+    the dgrad mask alone, for an x that is already a ReLU output.  All reproduce the
+    unfused nn.ReLU + layer bit for bit."""
+
+    SKIP_MASK = 1 << 8  # python-side flag, never passed to the library
 
     @staticmethod
     def forward(ctx, x, w, b, flags=0):
@@ -287,7 +291,8 @@ class _Deconv4s2(torch.autograd.Function):
         Cout = w.shape[1]
         wc = w.contiguous()
         small = Cout <= 4  # the RGB output layer: quad GEMM over the 3x3 neighbourhood
-        ok = _lib.LV_DECONV_RELU_IN if small else _lib.LV_DECONV_RELU_OUT
+        ok = ((_lib.LV_DECONV_RELU_IN | _lib.LV_DECONV_MASK_GX) if small
+              else (_lib.LV_DECONV_RELU_OUT | _Deconv4s2.SKIP_MASK))
         assert flags & ~ok == 0, f"flags {flags} not supported for Cout={Cout}"
         pre = "lv_deconv4s2_small_" if small else "lv_deconv4s2_"
         wt = torch.empty(getattr(_lib.load(), pre + "packed_weight_elems")(Cin), device=x.device,
@@ -297,8 +302,9 @@ class _Deconv4s2(torch.autograd.Function):
         st = _lib.stream()
         _lib.call(pre + "pack_weight_bf16", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
         _lib.call(pre + "fwd_bf16_ex", x.data_ptr(), wt.data_ptr(),
-                  None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, flags, st)
-        relu_out = bool(flags & _lib.LV_DECONV_RELU_OUT)
+                  None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout,
+                  flags & (_lib.LV_DECONV_RELU_IN | _lib.LV_DECONV_RELU_OUT), st)
+        relu_out = bool(flags & _lib.LV_DECONV_RELU_OUT) and not flags & _Deconv4s2.SKIP_MASK
         ctx.save_for_backward(x, wc, *((y,) if relu_out else ()))
         ctx.has_bias = b is not None
         ctx.flags = flags
@@ -311,7 +317,7 @@ class _Deconv4s2(torch.autograd.Function):
         N, Cin, H, W = x.shape
         Cout = w.shape[1]
         gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if ctx.flags & _lib.LV_DECONV_RELU_OUT:
+        if ctx.flags & _lib.LV_DECONV_RELU_OUT and not ctx.flags & _Deconv4s2.SKIP_MASK:
             gy = torch.ops.aten.threshold_backward(gy, ctx.saved_tensors[2], 0)
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         need_b = need_b and ctx.has_bias
@@ -346,13 +352,20 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
     relu_in / relu_out (plain attributes, not state): the layer computes
     layer(relu(x)) / relu(layer(x)) -- DeconvNet moves its nn.ReLU modules into the
     neighbouring layers this way (FUSED_RELU); the MFMA path fuses relu_out for Cout > 4
-    and relu_in for Cout <= 4 into the kernels, everything else applies F.relu."""
+    and relu_in for Cout <= 4 into the kernels, everything else applies F.relu.
+    input_is_relu: x is a ReLU output (relu(x) = x), so only the ReLU's backward mask
+    remains, in the RGB layer's dgrad epilogue; grad_masked_downstream (on the layer that
+    produced that x with relu_out): its consumer returns the masked gradient, so its own
+    backward skips the mask.  Either way the consumer's fallback path applies F.relu,
+    whose backward masks."""
 
     relu_in = False
     relu_out = False
+    input_is_relu = False
+    grad_masked_downstream = False
 
     def extra_repr(self):
-        fl = [n for n in ("relu_in", "relu_out") if getattr(self, n)]
+        fl = [n for n in ("relu_in", "relu_out", "input_is_relu", "grad_masked_downstream") if getattr(self, n)]
         return super().extra_repr() + "".join(f", {n}=True" for n in fl)
 
     def _mfma_ok(self, x):
@@ -368,15 +381,17 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
         bf16 = x.dtype == torch.bfloat16 or (
             torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
         if output_size is not None or not bf16 or not self._mfma_ok(x):
-            y = super().forward(F_.relu(x) if self.relu_in else x, output_size)
+            y = super().forward(F_.relu(x) if self.relu_in or self.input_is_relu else x, output_size)
             return F_.relu(y) if self.relu_out else y
         from .. import _lib
         small = self.out_channels <= 4
         flags = ((_lib.LV_DECONV_RELU_IN if self.relu_in and small else 0)
-                 | (_lib.LV_DECONV_RELU_OUT if self.relu_out and not small else 0))
+                 | (_lib.LV_DECONV_MASK_GX if self.input_is_relu and not self.relu_in and small else 0)
+                 | (_lib.LV_DECONV_RELU_OUT if self.relu_out and not small else 0)
+                 | (_Deconv4s2.SKIP_MASK if self.relu_out and self.grad_masked_downstream and not small else 0))
         with torch.autocast("cuda", enabled=False):
             xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            if self.relu_in and not small:
+            if (self.relu_in or self.input_is_relu) and not small:
                 xb = F_.relu(xb)
             y = _Deconv4s2.apply(xb, self.weight.to(torch.bfloat16),
                                  None if self.bias is None else self.bias.float(), flags)
@@ -490,9 +505,11 @@ class ConvNetBN(nn.Sequential):
 
 class DeconvNet(nn.Sequential):
     """1x1 -> 64x64 transposed-conv stack — nets.py:60-75.  With FUSED_RELU (and the MFMA
-    layers) the ReLUs after the 2nd and 3rd layers become the layers' relu_out and the
-    ReLU after the 4th becomes the RGB layer's relu_in (the kernels apply them); their
-    slots hold nn.Identity, so module indices and state_dict keys are the reference's."""
+    layers) the ReLUs after the 2nd, 3rd and 4th layers become those layers' relu_out
+    (their forward epilogues apply them); the 4th's backward mask moves into the RGB
+    layer's dgrad epilogue (input_is_relu / grad_masked_downstream), the other two masks
+    stay in the layers' own backward.  The ReLU slots hold nn.Identity, so module indices
+    and state_dict keys are the reference's."""
 
     def __init__(self, in_dims, hidden_dims, rgb=False):
         layers = [View(-1, in_dims, 1, 1), _convt(in_dims, hidden_dims, 4, 1, 0), nn.ReLU()]
@@ -500,11 +517,11 @@ class DeconvNet(nn.Sequential):
             layers += [_convt_s2(hidden_dims, hidden_dims, 4, 2, 1), nn.ReLU()]
         layers.append(_convt_s2(hidden_dims, 3 if rgb else 1, 4, 2, 1))
         if FUSED_RELU and MFMA_DECONV:
-            for i in (3, 5):  # layers 2, 3: relu_out
+            for i in (3, 5, 7):  # layers 2, 3, 4: relu_out
                 layers[i].relu_out = True
                 layers[i + 1] = nn.Identity()
-            layers[9].relu_in = True  # the RGB layer reads relu(layer 4's output)
-            layers[8] = nn.Identity()
+            layers[7].grad_masked_downstream = True
+            layers[9].input_is_relu = True
         super().__init__(*layers)
 
 

@@ -596,10 +596,39 @@ def test_mfma_deconv_backward_matches_autograd(gpu_device, N, Cin, Cout, H, W):
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
 
 
+def test_small_deconv_relu_in_bitwise(gpu_device):
+    """The RGB layer's LV_DECONV_RELU_IN (forward / wgrad stage max(x, 0), dgrad masks gx by
+    x > 0) and LV_DECONV_MASK_GX (the mask alone, on an x that is a ReLU output) against
+    relu(x) through the plain kernels and aten's threshold_backward: bit for bit."""
+    from lie_vae import _lib
+    from lie_vae.experiments.nets import _Deconv4s2
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(3, 200, 17, 16, generator=g).to(torch.bfloat16).to(gpu_device)
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(200, 3, 4, 4, generator=g) * 0.05).to(torch.bfloat16).to(gpu_device)
+    b = torch.randn(3, generator=g).to(gpu_device)
+    gy = torch.randn(3, 3, 34, 32, generator=g).to(torch.bfloat16).to(gpu_device)
+    gy = gy.contiguous(memory_format=torch.channels_last)
+    res = {}
+    for tag, flags, pre in (("ref", 0, True), ("relu_in", _lib.LV_DECONV_RELU_IN, False),
+                            ("mask", _lib.LV_DECONV_MASK_GX, True)):
+        xi = (torch.relu(x) if pre else x).detach().requires_grad_(True)
+        wi, bi = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        y = _Deconv4s2.apply(xi, wi, bi, flags)
+        y.backward(gy)
+        gx = xi.grad
+        if tag == "ref":
+            gx = torch.ops.aten.threshold_backward(gx, torch.relu(x), 0)
+        res[tag] = (y.detach(), gx, wi.grad, bi.grad)
+    for tag in ("relu_in", "mask"):
+        for name, a, r in zip(("y", "gx", "gw", "gb"), res[tag], res["ref"]):
+            assert torch.equal(a, r), f"{tag}: {name}"
+
+
 def test_fused_relu_deconvnet_bitwise(gpu_device, monkeypatch):
     """DeconvNet with its ReLUs fused into the MFMA layers (nets.FUSED_RELU: relu_out on the
-    2nd / 3rd layers' forward epilogue, relu_in on the RGB layer -- max(x, 0) staged by its
-    forward and wgrad, gx masked by x > 0 in its dgrad epilogue) against the same network
+    2nd / 3rd / 4th layers' forward epilogue, the 4th's backward mask in the RGB layer's
+    dgrad epilogue) against the same network
     with plain nn.ReLU modules, bf16 autocast, channels-last: output and every parameter
     and input gradient bit for bit (ReLU commutes with the bf16 rounding; the masks are the
     same comparisons).  MIOpen (the 200 -> 200 layers' backward) is pinned to deterministic
@@ -613,7 +642,7 @@ def test_fused_relu_deconvnet_bitwise(gpu_device, monkeypatch):
         monkeypatch.setattr(nets, "FUSED_RELU", fused)
         mods.append(nets.DeconvNet(1210, 200, rgb=True).to(gpu_device).to(memory_format=torch.channels_last))
     mods[1].load_state_dict(mods[0].state_dict())
-    assert isinstance(mods[0][8], torch.nn.Identity) and mods[0][9].relu_in
+    assert isinstance(mods[0][8], torch.nn.Identity) and mods[0][9].input_is_relu
     assert isinstance(mods[1][8], torch.nn.ReLU)
     z = torch.randn(6, 1210, device=gpu_device)
     gy = torch.randn(6, 3, 64, 64, device=gpu_device)
