@@ -21,7 +21,8 @@ LV_EXTERN_BWD(10) LV_EXTERN_BWD(11) LV_EXTERN_BWD(12) LV_EXTERN_BWD(13) LV_EXTER
 LV_EXTERN_BWD(15) LV_EXTERN_BWD(16) LV_EXTERN_BWD(17) LV_EXTERN_BWD(18) LV_EXTERN_BWD(19)
 LV_EXTERN_BWD(20)
 
-// Shared-spectrum gradient: gF[e] = sum over the tile kernel's slabs.  One block per
+// Shared-spectrum gradient: gF[e] = sum over the tile kernel's slabs.  (Round-2 kernel,
+// kept for A/B as LV_BWD_REDUCE=1; action_bwd_reduce2_kernel below is the default.)  One block per
 // kBwdReduceCols consecutive elements, lane = (slab stream k, column); the block's 16
 // waves split the slabs into contiguous runs, and inside a run stream k takes every
 // kBwdReduceStreams-th slab (64-byte loads, unrolled).  Against one element per lane this
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(64 * kBwdReduceWaves) void action_bwd_reduce_kernel
   }
 }
 
-// Variant (A/B build only until measured): one block per COLS consecutive elements, 1024
+// The default since round 3: one block per COLS consecutive elements, 1024
 // threads = 1024/COLS slab streams per element; stream k sums slabs k, k + S, k + 2S, ...
 // (all of a thread's loads issued together), then the S partials of an element are
 // added by a fixed-order halving tree in LDS.  Deterministic; a different (fixed)
@@ -505,7 +506,10 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.stream = st;
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
-  static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", 0);  // A/B: 8 / 16 = reduce2 columns
+  // dF slab reduce: action_bwd_reduce2_kernel<16> by default (profiles/r03_bwd_reduce_ab.txt:
+  // 17.51 vs 17.89 us per lv_group_action_bwd call at batch 4,096, 9.63 vs 9.75 at 512,
+  // 191.0 vs 191.1 at 65,536); A/B: LV_BWD_REDUCE = 1 the round-2 kernel, 4 / 8 columns
+  static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", 16);
   if (kEnvReduce == 8) {
     hipLaunchKernelGGL(action_bwd_reduce2_kernel<8>, dim3(ceil_div(MC, 8)), dim3(1024), 0, st,
                        (const float*)workspace, gF, MC, b.gx);

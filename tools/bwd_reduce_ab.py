@@ -1,5 +1,7 @@
 """A/B of the shared-spectrum dF reduction of lv_group_action_bwd (A/B build knob
-LV_BWD_REDUCE: 0 = action_bwd_reduce_kernel, 4 / 8 / 16 = action_bwd_reduce2_kernel<COLS>).
+LV_BWD_REDUCE: 1 = action_bwd_reduce_kernel (round 2), 4 / 8 / 16 = action_bwd_reduce2_kernel<COLS>,
+16 the default since round 3; the first table, profiles/r03_bwd_reduce_ab.txt, was taken when 0 = the
+round-2 kernel was the default).
 Per variant (own process): us per lv_group_action_bwd call at batch B (graph-captured,
 bench.bench_action_bwd_kernel), gF against the default kernel (relative max error) and
 a repeat call bit for bit.
@@ -46,7 +48,7 @@ def main():
     os.makedirs("gpurun_out", exist_ok=True)
     for B in batches:
         ref = None
-        for knob in ("0", "16", "8", "4", "0"):
+        for knob in ("1", "16", "8", "4", "1"):
             path = f"gpurun_out/gF_{B}_{knob}.npy"
             env = dict(os.environ, LV_BWD_REDUCE=knob,
                        LIEVAE_HIP_LIB=os.path.abspath("lie-vae_amd/lie_vae/liblievae_hip_ab.so"))
