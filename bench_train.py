@@ -70,6 +70,9 @@ def main():
                     help="stride-2 ConvTranspose2d: MIOpen's transposed convolution, one 3x3 "
                          "convolution + pixel shuffle (nets.PHASE_DECONV), or the library's MFMA "
                          "kernel for bf16 channels-last (nets.MFMA_DECONV)")
+    ap.add_argument("--conv-dgrad", choices=["mfma", "miopen"], default="mfma",
+                    help="encoder Conv2d(4, 2, 1) input gradients on the library's transposed-conv "
+                         "kernel (nets.MFMA_CONV_DGRAD) or MIOpen")
     ap.add_argument("--fused-relu", choices=["on", "off"], default="on",
                     help="DeconvNet's ReLUs inside the MFMA deconv kernels (nets.FUSED_RELU)")
     ap.add_argument("--graph", action="store_true",
@@ -112,6 +115,7 @@ def main():
     nets.PHASE_DECONV = args.deconv == "phase"
     nets.MFMA_DECONV = args.deconv == "mfma"
     nets.FUSED_RELU = args.fused_relu == "on"
+    nets.MFMA_CONV_DGRAD = args.conv_dgrad == "mfma"
 
     torch.manual_seed(0)
     model = VAE(latent_mode="so3", decoder_mode="action", degrees=args.lmax, rep_copies=10,
@@ -161,7 +165,7 @@ def main():
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
                        "conv_gemm": args.conv_gemm, "bn": args.bn, "bias_grad": args.bias_grad,
-                       "deconv": args.deconv, "fused_relu": args.fused_relu,
+                       "deconv": args.deconv, "fused_relu": args.fused_relu, "conv_dgrad": args.conv_dgrad,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,

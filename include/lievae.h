@@ -201,9 +201,12 @@ int lv_fused_exp_action_fwd_repeat(const float* mu, const float* v, const float*
 /* ---- decoder ConvTranspose2d(Cin, Cout, 4, stride 2, padding 1) on MFMA (§8 f1) -----
  * Replaces the MIOpen transposed convolution behind nn.ConvTranspose2d.forward for the
  * DeconvNet upsampling layers (reference experiments/nets.py:60-75), bf16 NHWC in/out,
- * fp32 accumulate.  Cin % 8 == 0, Cout % 8 == 0, Cout <= 208.  The weight (Cin, Cout, 4, 4)
+ * fp32 accumulate.  Cin % 8 == 0, Cout % 4 == 0, Cout <= 208.  The weight (Cin, Cout, 4, 4)
  * bf16 is first repacked into lv_deconv4s2_packed_weight_elems(Cin) bf16 elements (four
- * output phases x 208 channels x 4*Cin taps); bias (Cout) fp32 or NULL. */
+ * output phases x 208 channels x 4*Cin taps, + 64 zero bytes); bias (Cout) fp32 or NULL.
+ * The same call computes the input gradient of Conv2d(Cout, Cin, 4, 2, 1) (the encoder's
+ * strided convolutions, nets.py:33-57): gx = conv_transpose2d(gy, W) with the Conv2d
+ * weight W (Cin_conv_out, Cout_conv_in, 4, 4) read as this layer's (Cin, Cout, 4, 4). */
 size_t lv_deconv4s2_packed_weight_elems(int Cin);
 int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, void* stream);
 int lv_deconv4s2_fwd_bf16(const void* x, const void* wt, const float* bias, void* y, int64_t N,

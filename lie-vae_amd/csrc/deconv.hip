@@ -406,16 +406,31 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
       }
     }
     __syncthreads();
-    for (int e = tid; e < SR * pieces; e += 512) {
-      const int row = e / pieces, q = e - row * pieces;
-      const int64_t m = m0 + pass * SR + row;
-      if (m >= a.M) continue;
-      const int b = (int)(m % a.W);
-      const int64_t na = m / a.W;
-      const int aa_ = (int)(na % a.H);
-      const int64_t n = na / a.H;
-      __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 8;
-      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + row * kBN + q * 8);
+    if (pieces * 8 == a.Cout) {
+      for (int e = tid; e < SR * pieces; e += 512) {
+        const int row = e / pieces, q = e - row * pieces;
+        const int64_t m = m0 + pass * SR + row;
+        if (m >= a.M) continue;
+        const int b = (int)(m % a.W);
+        const int64_t na = m / a.W;
+        const int aa_ = (int)(na % a.H);
+        const int64_t n = na / a.H;
+        __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 8;
+        *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + row * kBN + q * 8);
+      }
+    } else {  // Cout % 4 == 0: 8-byte pieces (e.g. an encoder conv's dgrad to 100 channels)
+      const int p4 = a.Cout / 4;
+      for (int e = tid; e < SR * p4; e += 512) {
+        const int row = e / p4, q = e - row * p4;
+        const int64_t m = m0 + pass * SR + row;
+        if (m >= a.M) continue;
+        const int b = (int)(m % a.W);
+        const int64_t na = m / a.W;
+        const int aa_ = (int)(na % a.H);
+        const int64_t n = na / a.H;
+        __hip_bfloat16* dst = a.y + (((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout) + q * 4;
+        *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(Cs + row * kBN + q * 4);
+      }
     }
   }
 }
@@ -1024,7 +1039,7 @@ int lv_deconv4s2_pack_weight_bf16(const void* w, void* wt, int Cin, int Cout, vo
   clear_error();
   LV_CHECK_ARG(w && wt, "null pointer");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
-  LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 8 == 0, "Cout must be a multiple of 8 in [8, %d] (got %d)", kBN, Cout);
+  LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 4 == 0, "Cout must be a multiple of 4 in [4, %d] (got %d)", kBN, Cout);
   LV_CHECK_ARG((int64_t)Cin * Cout * 16 < (1ll << 31), "weight too large");
   hipLaunchKernelGGL(deconv_pack_kernel, dim3(ceil_div(4 * kBN * (Cin / 2), 256)), dim3(256), 0, (hipStream_t)stream,
                      (const __hip_bfloat16*)w, (__hip_bfloat16*)wt, Cin, Cout);
@@ -1042,7 +1057,7 @@ static int deconv_fwd(const void* x, const void* wt, const float* bias, void* y,
   LV_CHECK_ARG((flags & ~LV_DECONV_RELU_OUT) == 0, "flags: only LV_DECONV_RELU_OUT for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
-  LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 8 == 0, "Cout must be a multiple of 8 in [8, %d] (got %d)", kBN, Cout);
+  LV_CHECK_ARG(Cout > 0 && Cout <= kBN && Cout % 4 == 0, "Cout must be a multiple of 4 in [4, %d] (got %d)", kBN, Cout);
   if (N == 0) return LV_OK;
   LV_CHECK_ARG(x && wt && y, "null pointer");
   const int64_t M = N * H * W;
@@ -1052,6 +1067,7 @@ static int deconv_fwd(const void* x, const void* wt, const float* bias, void* y,
   DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout,
                (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
   if (bm == 0) bm = kDeconvAutoBM;
+  LV_CHECK_ARG(Cout % 8 == 0 || (bm >= 2 && bm <= 5), "the v1 kernels need Cout %% 8 == 0 (got %d)", Cout);
   if (bm == 2) return launch_deconv_v2<2, false>(a, (hipStream_t)stream);
   if (bm == 3) return launch_deconv_v2<3, false>(a, (hipStream_t)stream);
   if (bm == 4) return launch_deconv_v2<2, true>(a, (hipStream_t)stream);

@@ -398,6 +398,75 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
             return F_.relu(y) if self.relu_out and small else y
 
 
+# The encoder's strided Conv2d(c_in, c_out, 4, 2, 1) backward-data on the library's MFMA
+# transposed-convolution kernel: gx = conv_transpose2d(gy, W, stride 2, padding 1) is exactly
+# lv_deconv4s2_fwd_bf16 with the Conv2d weight (c_out, c_in, 4, 4) read as a
+# ConvTranspose2d(c_out, c_in) weight.  MIOpen runs these dgrads at ~100-120 TFLOP/s
+# (profiles/r03_train_config3_bf16_fused_steady_kernels.txt, igemm_bwd).  Forward and the
+# weight / bias gradients stay on MIOpen.
+MFMA_CONV_DGRAD = True
+
+
+class _Conv4s2(torch.autograd.Function):
+    """y = conv2d(x, w, b, stride 2, padding 1), k = 4, bf16 channels-last: forward and
+    gw / gb by MIOpen (torch), gx by lv_deconv4s2_fwd_bf16 (fp32 accumulation, one bf16
+    rounding)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.conv2d(x, w, b, 2, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _lib
+        x, w = ctx.saved_tensors
+        N, ci, H, W = x.shape
+        co = w.shape[0]
+        gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        need_x, need_w, need_b = ctx.needs_input_grad
+        need_b = need_b and ctx.has_bias
+        gx = gw = gb = None
+        if need_x:
+            st = _lib.stream()
+            wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems(co), device=x.device,
+                             dtype=torch.bfloat16)
+            _lib.call("lv_deconv4s2_pack_weight_bf16", w.contiguous().data_ptr(), wt.data_ptr(), co, ci, st)
+            gx = torch.empty_like(x, memory_format=torch.channels_last)
+            _lib.call("lv_deconv4s2_fwd_bf16", gy.data_ptr(), wt.data_ptr(), None, gx.data_ptr(),
+                      N, H // 2, W // 2, co, ci, st)
+        if need_w or need_b:
+            _, gw, gb = torch.ops.aten.convolution_backward(
+                gy, x, w, [co] if need_b else None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                [False, need_w, need_b])
+        return gx, gw, gb
+
+
+class MfmaDgradConv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters / state_dict) whose k4 s2 p1 input gradient runs on the
+    library's MFMA transposed-convolution kernel for bf16 channels-last inputs (autocast
+    bf16, or bf16 tensors) with c_out % 8 == 0, c_in % 4 == 0, c_in <= 208 and even H, W;
+    everything else is nn.Conv2d."""
+
+    def _ok(self, x):
+        return (x.is_cuda and x.dim() == 4 and _cl(x) and x.requires_grad
+                and self.kernel_size == (4, 4) and self.stride == (2, 2) and self.padding == (1, 1)
+                and self.dilation == (1, 1) and self.groups == 1 and self.padding_mode == "zeros"
+                and self.out_channels % 8 == 0 and self.in_channels % 4 == 0
+                and self.in_channels <= 208 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
+
+    def forward(self, x):
+        bf16 = x.dtype == torch.bfloat16 or (
+            torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        if not bf16 or not self._ok(x):
+            return super().forward(x)
+        with torch.autocast("cuda", enabled=False):
+            xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            return _Conv4s2.apply(xb, self.weight.to(torch.bfloat16),
+                                  None if self.bias is None else self.bias.to(torch.bfloat16))
+
+
 class PhaseConvTranspose2d(nn.ConvTranspose2d):
     """ConvTranspose2d(c_in, c_out, 4, 2, 1) as ONE stride-1 3x3 convolution to 4·c_out
     channels followed by a pixel shuffle (sub-pixel decomposition): output pixel
@@ -477,7 +546,7 @@ def _down_stack(in_dims, hidden, out_dims, batch_norm):
     """64x64 -> 4x4 by four stride-2 4x4 convs (widths h, 2h, 4h, 8h), then 4x4 -> 1x1."""
     layers, c = [], in_dims
     for i, width in enumerate([hidden, hidden * 2, hidden * 4, hidden * 8]):
-        layers.append(nn.Conv2d(c, width, 4, 2, 1))
+        layers.append((MfmaDgradConv2d if MFMA_CONV_DGRAD else nn.Conv2d)(c, width, 4, 2, 1))
         if batch_norm and FUSED_BN_ACT:
             layers += [FusedBatchNormLeakyReLU(width, 0.2), nn.Identity()]
         else:

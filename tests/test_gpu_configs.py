@@ -596,6 +596,35 @@ def test_mfma_deconv_backward_matches_autograd(gpu_device, N, Cin, Cout, H, W):
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
 
 
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(3, 100, 200, 16, 16), (2, 200, 400, 8, 8), (2, 48, 96, 10, 6)])
+def test_mfma_conv_dgrad_matches_autograd(gpu_device, N, Cin, Cout, H, W):
+    """MfmaDgradConv2d (the encoder's Conv2d(c, 2c, 4, 2, 1)): gx from
+    lv_deconv4s2_fwd_bf16 with the Conv2d weight read as a transposed-convolution weight,
+    against float64 autograd of conv2d on the same bf16 x, w and gy (fp32 accumulation,
+    one bf16 rounding: 2^-8 |ref| + 1e-3 rms); forward and gw / gb are MIOpen's (2^-5 |ref|
+    + 1e-2 rms, as in test_mfma_deconv_backward_matches_autograd)."""
+    from lie_vae.experiments.nets import _Conv4s2
+    g = torch.Generator().manual_seed(N * 11 + Cin + H)
+    x = torch.randn(N, Cin, H, W, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 4, 4, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g).to(torch.bfloat16)
+    gy = torch.randn(N, Cout, H // 2, W // 2, generator=g).to(torch.bfloat16)
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.conv2d(xr, wr, br, 2, 1).backward(gy.double())
+    xd = x.to(gpu_device).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wd = w.to(gpu_device).requires_grad_(True)
+    bd = b.to(gpu_device).requires_grad_(True)
+    _Conv4s2.apply(xd, wd, bd).backward(gy.to(gpu_device).contiguous(memory_format=torch.channels_last))
+    for name, got, ref, rel, absr in (("gx", xd.grad, xr.grad, 2.0 ** -8, 1e-3),
+                                      ("gw", wd.grad, wr.grad, 2.0 ** -5, 1e-2),
+                                      ("gb", bd.grad, br.grad, 2.0 ** -5, 1e-2)):
+        assert got.shape == ref.shape, name
+        gd = got.double().cpu()
+        rms = ref.square().mean().sqrt()
+        bad = (gd - ref).abs() > rel * ref.abs() + absr * rms
+        assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
+
+
 def test_small_deconv_relu_in_bitwise(gpu_device):
     """The RGB layer's LV_DECONV_RELU_IN (forward / wgrad stage max(x, 0), dgrad masks gx by
     x > 0) and LV_DECONV_MASK_GX (the mask alone, on an x that is a ReLU output) against

@@ -34,6 +34,7 @@ for v in $VARIANTS; do
     bf16_phase) A="--amp bf16 --channels-last --bn native --deconv phase" ;;
     bf16_mfma) A="--amp bf16 --channels-last --bn native --deconv mfma" ;;
     bf16_norelu) A="--amp bf16 --channels-last --bn native --deconv mfma --fused-relu off" ;;
+    bf16_miodgrad) A="--amp bf16 --channels-last --bn native --deconv mfma --conv-dgrad miopen" ;;
     bf16_nbn2) A="--amp bf16 --channels-last --bn native" ;;
     f32_phase) A="--bn native --deconv phase" ;;
     f32_both) A="--bn native --bias-grad gemv" ;;
