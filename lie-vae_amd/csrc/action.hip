@@ -198,6 +198,7 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvTile = LV_KNOB("LV_TILE", 1);
   static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
   static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
+  static const int kEnvPrio = LV_KNOB("LV_TILE_PRIO", 2);      // wave priority phases (ActionArgs)
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
   const int Sw = 64 / a.C;
@@ -225,6 +226,7 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   a.Sw = Sw;
   a.write_through = (int64_t)a.n * a.MC * out_bytes <= kWriteThroughMaxBytes ? 1 : 0;
   if (kEnvWT >= 0) a.write_through = kEnvWT;
+  a.prio = kEnvPrio;
   p.tile = true;
   p.lds = lds;
   p.gx = (int)groups;
@@ -498,6 +500,8 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.a.Sw = b.Sw;
   p.a.transpose = transpose ? 1 : 0;
   p.a.fpitch = b.fpitch;
+  static const int kEnvBwdPrio = LV_KNOB("LV_BWD_PRIO", 0);  // A/B: 2 = prologue-priority phases
+  p.a.prio = kEnvBwdPrio;
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
   p.gx = b.gx;
   p.nseg = b.nseg;

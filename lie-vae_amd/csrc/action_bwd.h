@@ -48,6 +48,7 @@ struct ActionBwdArgs {
   int64_t groups;      // ceil(n / Sw); block b takes groups b, b + gridDim.x, ...
   int C, Sw, transpose;
   int fpitch;          // floats per wave-private spectrum slice in LDS
+  int prio;            // 2: group load + prologue at s_setprio 3, chain at 0 (A/B: 0 off)
   int seg_lo[kMaxSeg + 1];
 };
 
@@ -209,6 +210,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     const int Sv = (int)min((int64_t)Sw, a.n - s0);
     const bool active = j < Sv;
     const int nbytes = Sv * (int)MC * 4;
+    if (a.prio >= 2) __builtin_amdgcn_s_setprio(3);
     // 1. upstream-gradient tile: global -> LDS by LDS-DMA (global_load_lds, 16-byte body,
     //    4-byte head/tail), issued first thing.  No VGPR holds the tile in flight: the
     //    register-staged form kept 32 VGPRs of loads live across the prologue, which the
@@ -252,6 +254,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     block_sync_lds();
 
+    if (a.prio >= 2) __builtin_amdgcn_s_setprio(0);
     float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
     const float* tj = trig + min(j, Sw - 1) * kRow;
     const float* Fs = a.F + (s0 + min(j, Sv - 1)) * a.Fstride + c;  // per-sample spectrum

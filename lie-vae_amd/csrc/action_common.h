@@ -26,6 +26,8 @@ struct ActionArgs {
   int C, Sw, transpose;
   int fpitch;           // tile kernel: floats per wave-private spectrum slice in LDS
   int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores, 2 = plain (A/B)
+  int prio;             // tile kernel wave priority: 2 = prologue at s_setprio 3, chain at 0
+                        // (default); A/B: 0 off, 1 flush at 3, 3 = 2 + flush at 2
   int seg_lo[kMaxSeg + 1];
 };
 

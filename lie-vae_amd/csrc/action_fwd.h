@@ -293,6 +293,13 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   float* const Fall = FT ? reinterpret_cast<float*>(stage_b) + (Sw - 1) * MC : trig + Sw * kRow;
   float* Fw = Fall + (CT > 0 ? rows_lo * C : wave * a.fpitch);
   // 1. prologue task (sample jt, slot q); the host guarantees 3*Sw <= blockDim.x
+  // Wave priority (a.prio, the plan's default 2): the prologue (v / mu loads, exp -> ZYZ,
+  // multiples, spectrum staging) issues at s_setprio 3 and the chain at 0, so on a CU that
+  // holds blocks in different phases a new block's loads start ahead of the other blocks'
+  // FMA streams (tools/gpu_fwd_knobs.sh, profiles/r03_fwd_prio_ab.txt: batch 16,384
+  // 20.96 -> 18.27 us, 65,536 63.6 -> 61.1, 262,144 256 -> 252; 4,096, where every block
+  // starts at once, unchanged).  1 / 3: A/B variants with the flush raised.
+  if (a.prio >= 2) __builtin_amdgcn_s_setprio(3);
   const int tid = (int)threadIdx.x;
   const bool task = tid < 3 * Sw;
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
@@ -338,6 +345,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   }
   block_sync_lds();
 
+  if (a.prio >= 2) __builtin_amdgcn_s_setprio(0);
   OutT* st_lane = reinterpret_cast<OutT*>(stage_b) + j * MC + c;
   const float* tj = trig + min(j, Sw - 1) * kRow;
   // spectrum column: LDS slice, or global (FG)
@@ -366,6 +374,8 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     }
   });
   block_sync_lds();
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(3);  // A/B: the flush ahead of other waves' chains
+  else if (a.prio == 3) __builtin_amdgcn_s_setprio(2);
   tile_flush_rt<OutT>(gout, stage_b, mis, Sv * (int)MC * (int)sizeof(OutT), a.write_through);
 }
 

@@ -358,7 +358,9 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
   for (int ks = 0; ks < nk; ++ks) {
     const int stage = ks % S;
     vm_wait(per * min(S - 2, nk - 1 - ks));  // this wave's pieces of step ks have landed
-    __syncthreads();                           // everyone's have; stage (ks - 1) % S is free
+    // everyone's have; stage (ks - 1) % S is free.  Not __syncthreads(): its fence waits for
+    // vmcnt(0), i.e. for the DMA of the steps still in flight, which undoes the ring.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (ks + S - 1 < nk) issue(ks + S - 1, (ks + S - 1) % S);
     const __hip_bfloat16* As = smem + stage * (T::kA + T::kB);
     const __hip_bfloat16* Bs = As + T::kA;

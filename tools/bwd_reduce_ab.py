@@ -48,14 +48,16 @@ def main():
     os.makedirs("gpurun_out", exist_ok=True)
     for B in batches:
         ref = None
-        for knob in ("1", "16", "8", "4", "1"):
-            path = f"gpurun_out/gF_{B}_{knob}.npy"
-            env = dict(os.environ, LV_BWD_REDUCE=knob,
+        knobs = os.environ.get("AB_KNOBS", "LV_BWD_REDUCE=1,LV_BWD_REDUCE=16,LV_BWD_REDUCE=8,LV_BWD_REDUCE=4,LV_BWD_REDUCE=1")
+        for kv in knobs.split(","):
+            name, knob = kv.split("=")
+            path = f"gpurun_out/gF_{B}_{name}_{knob}.npy"
+            env = dict(os.environ, **{name: knob},
                        LIEVAE_HIP_LIB=os.path.abspath("lie-vae_amd/lie_vae/liblievae_hip_ab.so"))
             r = subprocess.run([sys.executable, "-c", CHILD, str(B), path], env=env,
                                capture_output=True, text=True, timeout=120)
             if r.returncode != 0:
-                print(B, knob, "rc", r.returncode, r.stderr[-600:], flush=True)
+                print(B, name, knob, "rc", r.returncode, r.stderr[-600:], flush=True)
                 return 1
             d = json.loads(r.stdout.strip().splitlines()[-1])
             import numpy as np
@@ -63,7 +65,7 @@ def main():
             if ref is None:
                 ref = gF
             err = float(np.abs(gF - ref).max() / np.abs(ref).max())
-            print(f"B={B:6d} reduce={knob:>2}: {d['us']:7.2f} us/call  repeat bitwise {d['repeat_bitwise']}"
+            print(f"B={B:6d} {name}={knob:>2}: {d['us']:7.2f} us/call  repeat bitwise {d['repeat_bitwise']}"
                   f"  max |gF - default| / max|gF| {err:.2e}", flush=True)
     return 0
 

@@ -19,7 +19,8 @@ print(f'{sys.argv[1]:>14}  B4096 {d.get("us_per_launch_events", 0):6.2f} us  {sw
 PY
 }
 run base
-run wt2 LV_TILE_WT=2
+run prio0 LV_TILE_PRIO=0
+run prio3 LV_TILE_PRIO=3
 run base2
 # config 5 (l = 20, B = 8192, bf16 out): one-shot tile kernel vs the persistent one
 run_c5() {
@@ -34,4 +35,5 @@ print(f'{sys.argv[1]:>14}  B8192 {d.get("us_per_launch_events", 0):6.2f} us  {sw
 PY
 }
 run_c5 c5base
+run_c5 c5prio0 LV_TILE_PRIO=0
 run_c5 c5base2
