@@ -269,7 +269,8 @@ int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd
                                    int flags, void* stream);
 /* Same with an explicit kernel variant (A/B): 0 = the default, 128 / 256 = v1 (register-
  * staged double buffer) with that pixel-tile height, 2 / 3 = v2 (LDS-DMA ring of that many
- * stages, 4 x 2 wave tiling), 4 / 5 = v2 with 2 / 3 stages and XCD-grouped phases. */
+ * stages, 4 x 2 wave tiling), 4 / 5 = v2 with 2 / 3 stages and XCD-grouped phases, 6 / 7 =
+ * the same with 128-row block tiles (2 x 4 waves; 6 is the default). */
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y,
                                int64_t N, int H, int W, int Cin, int Cout, int bm, void* stream);
 

@@ -252,12 +252,17 @@ __global__ __launch_bounds__(BM * 2) void deconv_mfma_kernel(DeconvArgs a) {
 // (chunk ^ (row >> 2) & 3): the 16 rows of a fragment read fall in 16 distinct 4-bank
 // groups.  Taps outside the image read 64 zero bytes kept after the packed weight.  Same
 // MFMA sequence per output element as v1: bitwise equal.
-constexpr int kV2BM = 256;
-constexpr int kV2NW = 7;                       // channel tiles per wave (wn = 1: 6)
-template <int S>
+// BM = 256: 4 x 2 waves (64 rows x 7 | 6 channel tiles), 159 VGPRs, one block per CU;
+// BM = 128: 2 x 4 waves (64 rows x 3 | 3 | 3 | 4 tiles), for two blocks per CU.
+template <int S, int BM = 256>
 struct DeconvV2 {
-  static constexpr int kA = kV2BM * kBK, kB = kBN * kBK;  // bf16 per stage
-  static constexpr size_t kLds = (size_t)S * (kA + kB) * 2;  // S = 2: 59,392 B, 3: 89,088 B
+  static constexpr int kWM = BM / 64, kWN = 8 / kWM;                // wave grid
+  static constexpr int kNW = (kNT + kWN - 1) / kWN;                  // max channel tiles per wave
+  static constexpr int kAI = BM / 128;                               // A DMA instructions per wave
+  static constexpr int kSR = BM / 2;                                 // epilogue rows per pass
+  static constexpr int kA = BM * kBK, kB = kBN * kBK;                // bf16 per stage
+  static constexpr size_t kLds = (size_t)S * (kA + kB) * 2;          // BM 256, S = 2: 59,392 B
+  static_assert((size_t)kSR * kBN * 2 <= kLds, "epilogue stage fits the ring");
 };
 __device__ __forceinline__ int v2_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 __device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n wave-uniform
@@ -275,14 +280,16 @@ __device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n wave-
 // XCD: 1-D grid whose consecutive block ids are dealt round-robin over the 8 XCDs; the four
 // phases of a pixel tile get ids b, b + 8, b + 16, b + 24, i.e. the same XCD at about the
 // same time, so the tile's input pixels come from HBM into that XCD's L2 once, not 4 times.
-template <int S, bool XCD>
+template <int S, bool XCD, int BM = 256>
 __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
-  using T = DeconvV2<S>;
+  using T = DeconvV2<S, BM>;
+  constexpr int kV2BM = BM, kV2NW = T::kNW;
   extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / T::kWN, wn = wave % T::kWN;
+  const int t0 = wn * kNT / T::kWN, ntw = (wn + 1) * kNT / T::kWN - t0;  // this wave's channel tiles
   int p, tile;
   if constexpr (XCD) {
     const int bid = (int)blockIdx.x, slot = bid >> 3;
@@ -300,12 +307,12 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
   const __hip_bfloat16* wtp = a.wt + (int64_t)p * kBN * K;
   const __hip_bfloat16* zero16 = a.wt + (int64_t)4 * kBN * K;
   const int lrow = lane >> 2, lslot = lane & 3;
-  // A DMA: rows 32 wave + 16 i + lrow (i = 0, 1)
-  int64_t abase[2];
-  int aa[2], ab[2], achunk[2];
+  // A DMA: rows (BM / 8) wave + 16 i + lrow (i < kAI)
+  int64_t abase[T::kAI];
+  int aa[T::kAI], ab[T::kAI], achunk[T::kAI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 32 * wave + 16 * i + lrow;
+  for (int i = 0; i < T::kAI; ++i) {
+    const int row = (BM / 8) * wave + 16 * i + lrow;
     achunk[i] = v2_swz(row, lslot);
     const int64_t m = m0 + row;
     if (m < a.M) {
@@ -325,14 +332,14 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
     __hip_bfloat16* As = smem + stage * (T::kA + T::kB);
     __hip_bfloat16* Bs = As + T::kA;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < T::kAI; ++i) {
       const int k0 = ks * kBK + achunk[i] * 8;
       const int t = k0 / a.Cin, c = k0 - t * a.Cin;
       const int ia = aa[i] + r - 1 + (t >> 1), ib = ab[i] + s - 1 + (t & 1);
       const __hip_bfloat16* src = (abase[i] >= 0 && ia >= 0 && ia < a.H && ib >= 0 && ib < a.W)
                                       ? a.x + ((abase[i] + ia) * a.W + ib) * a.Cin + c
                                       : zero16;
-      __builtin_amdgcn_global_load_lds(src, as_lds(As + (32 * wave + 16 * i) * kBK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, as_lds(As + ((BM / 8) * wave + 16 * i) * kBK), 16, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -352,9 +359,8 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
 #pragma unroll
   for (int st = 0; st < S - 1; ++st)
     if (st < nk) issue(st, st);
-  const int per = 2 + nbg;  // DMA instructions per stage of this wave
+  const int per = T::kAI + nbg;  // DMA instructions per stage of this wave
   const int fr = lane & 15, kc = lane >> 4;
-  const int ntw = wn == 0 ? kV2NW : kNT - kV2NW;
   for (int ks = 0; ks < nk; ++ks) {
     const int stage = ks % S;
     vm_wait(per * min(S - 2, nk - 1 - ks));  // this wave's pieces of step ks have landed
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
 #pragma unroll
     for (int j = 0; j < kV2NW; ++j) {
       if (j < ntw) {
-        const int row = (wn * kV2NW + j) * 16 + fr;
+        const int row = (t0 + j) * 16 + fr;
         const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bs + row * kBK + v2_swz(row, kc) * 8);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -386,7 +392,7 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
   const int cq = (lane >> 4) * 4;
   const int pieces = a.Cout / 8;
   const int H2 = 2 * a.H, W2 = 2 * a.W;
-  constexpr int SR = 128;
+  constexpr int SR = T::kSR;
 #pragma unroll
   for (int pass = 0; pass < kV2BM / SR; ++pass) {
     __syncthreads();
@@ -394,7 +400,7 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
 #pragma unroll
       for (int j = 0; j < kV2NW; ++j) {
         if (j < ntw) {
-          const int o = (wn * kV2NW + j) * 16 + fr;
+          const int o = (t0 + j) * 16 + fr;
           const float bo = (a.bias && o < a.Cout) ? a.bias[o] : 0.f;
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
@@ -1006,21 +1012,23 @@ __global__ __launch_bounds__(kCsThreads) void channel_sum_part_kernel(const __hi
 
 using namespace lv;
 
-// default forward variant: v2, 2-stage LDS-DMA ring, XCD-grouped phases (batch 512, 200 -> 200:
-// 36 / 72 / 282 us at H = 4 / 8 / 16 against v1's 43 / 88 / 344, bitwise equal;
-// profiles/r03_deconv_v2.txt)
-constexpr int kDeconvAutoBM = 4;
+// default forward variant: v2 with 128-row block tiles (2 x 4 waves, 104 VGPRs: two blocks
+// per CU, so one block's epilogue stores overlap the other's MFMAs), 2-stage LDS-DMA ring,
+// XCD-grouped phases.  Batch 512, 200 -> 200 at H = 4 / 8 / 16: 26 / 65 / 260 us against
+// 256-row tiles' 38 / 74 / 284 and v1's 43 / 88 / 344, all bitwise equal
+// (profiles/r03_deconv_v2.txt).
+constexpr int kDeconvAutoBM = 6;
 
 namespace {
-template <int S, bool XCD>
+template <int S, bool XCD, int BM = 256>
 int launch_deconv_v2(const DeconvArgs& a, hipStream_t st) {
-  const int64_t tiles = (a.M + kV2BM - 1) / kV2BM;
+  const int64_t tiles = (a.M + BM - 1) / BM;
   if constexpr (XCD)
-    hipLaunchKernelGGL((deconv_mfma2_kernel<S, true>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
-                       DeconvV2<S>::kLds, st, a);
+    hipLaunchKernelGGL((deconv_mfma2_kernel<S, true, BM>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
+                       (DeconvV2<S, BM>::kLds), st, a);
   else
-    hipLaunchKernelGGL((deconv_mfma2_kernel<S, false>), dim3((unsigned)tiles, 4), dim3(512), DeconvV2<S>::kLds,
-                       st, a);
+    hipLaunchKernelGGL((deconv_mfma2_kernel<S, false, BM>), dim3((unsigned)tiles, 4), dim3(512),
+                       (DeconvV2<S, BM>::kLds), st, a);
   LV_RETURN_LAUNCH("deconv_mfma2_kernel");
 }
 template <int BM>
@@ -1064,16 +1072,18 @@ static int deconv_fwd(const void* x, const void* wt, const float* bias, void* y,
   LV_CHECK_ARG(x && wt && y, "null pointer");
   const int64_t M = N * H * W;
   LV_CHECK_ARG((M + 127) / 128 <= 0x7fffffff, "batch too large");
-  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256 || (bm >= 2 && bm <= 5),
+  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256 || (bm >= 2 && bm <= 7),
                "variant must be 0 (auto), 128 / 256 (v1 tile rows) or 2 / 3 (v2 stages), 4 / 5 (+ XCD order)");
   DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout,
                (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
   if (bm == 0) bm = kDeconvAutoBM;
-  LV_CHECK_ARG(Cout % 8 == 0 || (bm >= 2 && bm <= 5), "the v1 kernels need Cout %% 8 == 0 (got %d)", Cout);
+  LV_CHECK_ARG(Cout % 8 == 0 || (bm >= 2 && bm <= 7), "the v1 kernels need Cout %% 8 == 0 (got %d)", Cout);
   if (bm == 2) return launch_deconv_v2<2, false>(a, (hipStream_t)stream);
   if (bm == 3) return launch_deconv_v2<3, false>(a, (hipStream_t)stream);
   if (bm == 4) return launch_deconv_v2<2, true>(a, (hipStream_t)stream);
   if (bm == 5) return launch_deconv_v2<3, true>(a, (hipStream_t)stream);
+  if (bm == 6) return launch_deconv_v2<2, true, 128>(a, (hipStream_t)stream);
+  if (bm == 7) return launch_deconv_v2<3, true, 128>(a, (hipStream_t)stream);
   return bm == 256 ? launch_deconv<256>(a, (hipStream_t)stream) : launch_deconv<128>(a, (hipStream_t)stream);
 }
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
