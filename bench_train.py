@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--conv-dgrad", choices=["mfma", "miopen"], default="mfma",
                     help="encoder Conv2d(4, 2, 1) input gradients on the library's transposed-conv "
                          "kernel (nets.MFMA_CONV_DGRAD) or MIOpen")
+    ap.add_argument("--adam", choices=["fused", "foreach"], default="fused",
+                    help="torch.optim.Adam implementation (DPTrainer fused_adam)")
     ap.add_argument("--fused-relu", choices=["on", "off"], default="on",
                     help="DeconvNet's ReLUs inside the MFMA deconv kernels (nets.FUSED_RELU)")
     ap.add_argument("--graph", action="store_true",
@@ -127,7 +129,7 @@ def main():
         return bench_iwae(args, model, env, dev)
     trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5,
                         amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
-                        graph=args.graph)
+                        graph=args.graph, fused_adam=args.adam == "fused")
     B = args.global_batch // world
     g = torch.Generator(device="cpu").manual_seed(100 + rank)
     x = torch.rand(B, 3, 64, 64, generator=g).to(dev)
@@ -165,7 +167,7 @@ def main():
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
                        "conv_gemm": args.conv_gemm, "bn": args.bn, "bias_grad": args.bias_grad,
-                       "deconv": args.deconv, "fused_relu": args.fused_relu, "conv_dgrad": args.conv_dgrad,
+                       "deconv": args.deconv, "fused_relu": args.fused_relu, "conv_dgrad": args.conv_dgrad, "adam": args.adam,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,
                        "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,

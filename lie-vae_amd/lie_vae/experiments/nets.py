@@ -339,10 +339,21 @@ class _Deconv4s2(torch.autograd.Function):
                       None if wd is None else wd.data_ptr(), None if gx is None else gx.data_ptr(),
                       None if gw is None else gw.data_ptr(), None if gb is None else gb.data_ptr(),
                       None if ws is None else ws.data_ptr(), N, H, W, Cin, Cout, ctx.flags, st)
-            return gx, (gw if need_w else None), gb, None
+            return gx, (_like(gw, w) if need_w else None), gb, None
         gx, gw, _ = torch.ops.aten.convolution_backward(
             gy, x, w, None, [2, 2], [1, 1], [1, 1], True, [0, 0], 1, [need_x, need_w, False])
-        return gx, gw, (_channel_sum(gy) if need_b else None), None
+        return gx, _like(gw, w), (_channel_sum(gy) if need_b else None), None
+
+
+def _like(g, w):
+    """A weight gradient in its parameter's memory format (a channels-last model keeps
+    channels-last weights): AccumulateGrad then stores it as is, and the optimizer sees
+    params and grads of one layout -- the condition for torch.optim's foreach / fused
+    Adam paths (otherwise Adam falls back to one chain of kernels per tensor)."""
+    if g is None or g.stride() == w.stride():
+        return g
+    return g.contiguous(memory_format=torch.channels_last) if w.is_contiguous(
+        memory_format=torch.channels_last) else g.contiguous()
 
 
 class MfmaConvTranspose2d(nn.ConvTranspose2d):
@@ -440,7 +451,7 @@ class _Conv4s2(torch.autograd.Function):
             _, gw, gb = torch.ops.aten.convolution_backward(
                 gy, x, w, [co] if need_b else None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
                 [False, need_w, need_b])
-        return gx, gw, gb
+        return gx, _like(gw, w), gb
 
 
 class MfmaDgradConv2d(nn.Conv2d):

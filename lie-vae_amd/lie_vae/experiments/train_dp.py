@@ -150,7 +150,7 @@ class DPTrainer:
     def __init__(self, model, lr=1e-3, weight_decay=0.0, clip_grads=1e-5, beta=1.0,
                  elbo_samples=1, bucket_bytes=32 << 20, group=None, broadcast=True,
                  control=None, control_p=1, selective_clip=False, nan_check=False,
-                 amp_dtype=None, graph=False, sync_bn=False):
+                 amp_dtype=None, graph=False, sync_bn=False, fused_adam=None):
         if sync_bn and dist.is_initialized() and dist.get_world_size(group) > 1:
             from .nets import to_sync_batchnorm
             model = to_sync_batchnorm(model, process_group=group)
@@ -169,8 +169,13 @@ class DPTrainer:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, src=0, group=group)
         self.ar = BucketedAllReduce(model.parameters(), bucket_bytes=bucket_bytes, group=group)
+        # fused Adam (one kernel per dtype / device / layout group instead of the foreach
+        # kernels' chain) for device parameters; fused_adam=False keeps torch's default
+        # (foreach; an explicit fused=False would select the per-tensor loop)
+        if fused_adam is None:
+            fused_adam = all(p.is_cuda for p in model.parameters())
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay,
-                                    capturable=graph)
+                                    capturable=graph, fused=True if fused_adam else None)
         self._graph = None
 
     def loss(self, x, eps=None, beta=1.0):

@@ -35,6 +35,7 @@ for v in $VARIANTS; do
     bf16_mfma) A="--amp bf16 --channels-last --bn native --deconv mfma" ;;
     bf16_norelu) A="--amp bf16 --channels-last --bn native --deconv mfma --fused-relu off" ;;
     bf16_miodgrad) A="--amp bf16 --channels-last --bn native --deconv mfma --conv-dgrad miopen" ;;
+    bf16_foreach) A="--amp bf16 --channels-last --bn native --deconv mfma --adam foreach" ;;
     bf16_nbn2) A="--amp bf16 --channels-last --bn native" ;;
     f32_phase) A="--bn native --deconv phase" ;;
     f32_both) A="--bn native --bias-grad gemv" ;;
