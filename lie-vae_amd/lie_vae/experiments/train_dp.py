@@ -49,7 +49,12 @@ class BucketedAllReduce:
             buf = torch.zeros(sum(p.numel() for p in plist), dtype=dtype, device=plist[0].device)
             off = 0
             for p in plist:
-                p.grad = buf[off:off + p.numel()].view_as(p)
+                # the gradient view keeps its parameter's strides (a channels-last model's
+                # 4-D weights): same layout as the parameter and its Adam state, which
+                # torch's foreach / fused optimizer kernels require (else per-tensor loops)
+                flat = buf[off:off + p.numel()]
+                dense = p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))
+                p.grad = flat.as_strided(p.shape, p.stride()) if dense else flat.view_as(p)
                 self.owner[p] = bi
                 off += p.numel()
             self.state.append({"buf": buf, "left": len(plist), "handle": None})
