@@ -144,41 +144,53 @@ __global__ __launch_bounds__(kBnThreads) void bn_reduce_part_kernel(const __hip_
   }
 }
 
-// Fixed-order sum of the block partials (64 channels per block, 4 slices of blocks,
-// 4-way unrolled), then the per-channel epilogue in slice 0.
+// Fixed-order sum of the block partials: 64 channels per block, 16 slices of blocks (slice sl
+// takes blocks sl, sl + 16, ..., 4-way unrolled), the 16 slice sums added by a fixed
+// halving tree, then the per-channel epilogue in slice 0.  (Round 3: 16 slices instead of 4
+// -- the kernel runs on ceil(C / 64) blocks only, so its time is the partials' load latency.)
 //   MODE 0: batch mean / biased var -> save_mean, save_invstd, running stats, coef = [a | b]
 //   MODE 1: ggamma, gbeta and coef2 = [gamma·invstd | sum gz / P | sum gz·xhat / P]
+constexpr int kBnFinSlices = 16;
 template <int MODE>
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, int nblk, int C, int64_t P,
+__global__ __launch_bounds__(64 * kBnFinSlices) void bn_finalize_kernel(const float* part, int nblk, int C, int64_t P,
                                                           const __hip_bfloat16* x, const float* gamma,
                                                           const float* beta, float eps, float momentum,
                                                           float* running_mean, float* running_var, float* save_mean,
                                                           float* save_invstd, float* coef, float* ggamma,
                                                           float* gbeta) {
-  __shared__ float red[2][4][64];
+  constexpr int SL = kBnFinSlices;
+  __shared__ float red[2][SL][64];
   const int t = (int)threadIdx.x, el = t & 63, sl = t >> 6;
   const int c = blockIdx.x * 64 + el;
   float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     int b = sl;
-    for (; b + 12 < nblk; b += 16) {
+    for (; b + 3 * SL < nblk; b += 4 * SL) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a1[u] += part[(int64_t)(b + 4 * u) * 2 * C + c];
-        a2[u] += part[(int64_t)(b + 4 * u) * 2 * C + C + c];
+        a1[u] += part[(int64_t)(b + SL * u) * 2 * C + c];
+        a2[u] += part[(int64_t)(b + SL * u) * 2 * C + C + c];
       }
     }
-    for (; b < nblk; b += 4) {
+    for (; b < nblk; b += SL) {
       a1[0] += part[(int64_t)b * 2 * C + c];
       a2[0] += part[(int64_t)b * 2 * C + C + c];
     }
   }
   red[0][sl][el] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
   red[1][sl][el] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+#pragma unroll
+  for (int h = SL / 2; h >= 1; h >>= 1) {
+    __syncthreads();
+    if (sl < h) {
+      red[0][sl][el] += red[0][sl + h][el];
+      red[1][sl][el] += red[1][sl + h][el];
+    }
+  }
   __syncthreads();
   if (sl != 0 || c >= C) return;
-  const float S1 = (red[0][0][el] + red[0][1][el]) + (red[0][2][el] + red[0][3][el]);
-  const float S2 = (red[1][0][el] + red[1][1][el]) + (red[1][2][el] + red[1][3][el]);
+  const float S1 = red[0][0][el];
+  const float S2 = red[1][0][el];
   const float n = (float)P;
   const float gm = gamma ? gamma[c] : 1.f;
   if (MODE == 0) {
@@ -324,7 +336,7 @@ int lv_bn_lrelu_fwd_bf16(const void* x, const float* gamma, const float* beta, f
     hipLaunchKernelGGL(bn_reduce_part_kernel<0>, dim3(geo.nblk), dim3(kBnThreads), 0, st, (const __hip_bfloat16*)x,
                        (const __hip_bfloat16*)nullptr, (const float*)nullptr, slope, geo, ws);
     LV_CHECK_LAUNCH("bn_reduce_part_kernel<0>");
-    hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(ceil_div(C, 64)), dim3(256), 0, st, ws, geo.nblk, C, P,
+    hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(ceil_div(C, 64)), dim3(64 * kBnFinSlices), 0, st, ws, geo.nblk, C, P,
                        (const __hip_bfloat16*)x, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
                        save_invstd, coef, (float*)nullptr, (float*)nullptr);
     LV_CHECK_LAUNCH("bn_finalize_kernel<0>");
@@ -356,7 +368,7 @@ int lv_bn_lrelu_bwd_bf16(const void* g, const void* x, const float* gamma, const
   hipLaunchKernelGGL(bn_reduce_part_kernel<1>, dim3(geo.nblk), dim3(kBnThreads), 0, st, (const __hip_bfloat16*)x,
                      (const __hip_bfloat16*)g, (const float*)coef, slope, geo, ws);
   LV_CHECK_LAUNCH("bn_reduce_part_kernel<1>");
-  hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(ceil_div(C, 64)), dim3(256), 0, st, ws, geo.nblk, C, P,
+  hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(ceil_div(C, 64)), dim3(64 * kBnFinSlices), 0, st, ws, geo.nblk, C, P,
                      (const __hip_bfloat16*)x, gamma, beta, 0.f, 0.f, (float*)nullptr, (float*)nullptr,
                      (float*)save_mean, (float*)save_invstd, coef + 4 * C, ggamma, gbeta);
   LV_CHECK_LAUNCH("bn_finalize_kernel<1>");
