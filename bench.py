@@ -318,12 +318,22 @@ def main():
     raw_per_launch_s = gpu_ms / 1e3 / args.steps
     per_launch_s, t1_us = raw_per_launch_s, None
     if args.steps >= 10:
-        g1 = graph_of(1, False, False) if args.launch == "graph" else None
+        # t_1 is bracketed exactly as t_K was: stream events around one replay, or (with
+        # --events-in-graph) event nodes inside a one-launch graph
+        if args.launch == "graph" and events_in_graph:
+            g1 = graph_of(1, True, True)
+        else:
+            g1 = graph_of(1, False, False) if args.launch == "graph" else None
         if g1 is not None:
             g1.replay()
         ts = []
         for _ in range(5):
             torch.cuda.synchronize(dev)
+            if events_in_graph:
+                g1.replay()
+                torch.cuda.synchronize(dev)
+                ts.append(ev0.elapsed_time(ev1) / 1e3)
+                continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             if g1 is not None:
@@ -400,11 +410,19 @@ def main():
     if not args.no_fwd_bwd and rank == 0 and args.dtype == "f32":
         fwd_bwd = bench_fwd_bwd(v, F, L, dev, stream)
 
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", f"traffic_B{B}_L{L}_C{C}_{args.dtype}.json")
+    # HBM traffic per launch is NOT measured in this run (PMC counters need their own
+    # rocprofv3 --pmc passes, tools/gpu_prof.sh): it is read from the committed summary of
+    # those passes for this exact shape, and the line says so ("traffic_source")
+    traffic, traffic_source = None, None
+    tname = f"traffic_B{B}_L{L}_C{C}_{args.dtype}.json"
+    tpath = os.path.join(REPO, "profiles", tname)
     if os.path.exists(tpath):
         with open(tpath) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)
+        traffic = tj.get("hbm_bytes_per_launch")
+        traffic_source = (f"profiles/{tname}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                          f"({tj.get('measured', 'committed earlier')}), read from the file, not "
+                          "measured in this run")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -433,13 +451,16 @@ def main():
                        "launch": args.launch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "algorithmic_bytes_per_launch": abytes,
                          "us_per_launch_events": per_launch_s * 1e6,
                          "us_per_launch_events_raw": raw_per_launch_s * 1e6,
                          "us_one_launch_bracket": t1_us,
-                         "per_launch_rule": "(t_K - t_1) / (K - 1): HIP events on the launch "
-                                            "stream around the K timed launches and around one "
-                                            "launch (median of 5)",
+                         "per_launch_rule": "MARGINAL per-launch time (t_K - t_1) / (K - 1): "
+                                            "HIP events bracket the K timed launches and, the "
+                                            "same way, one launch (median of 5); the fixed "
+                                            "submission cost both brackets hold cancels. The "
+                                            "raw t_K / K is us_per_launch_events_raw",
                          "events": "graph nodes" if events_in_graph else "stream",
                          "cache": "hot (back-to-back launches)"},
             "cache_cold": cache_cold,

@@ -60,16 +60,9 @@ def main():
                     help="run the two GEMM-shaped layers (decoder 1x1->4x4 ConvTranspose2d, "
                          "encoder 4x4->1x1 head) as addmm on hipBLASLt (on) or through MIOpen "
                          "(off); nets.GEMM_LAYERS")
-    ap.add_argument("--bn", choices=["miopen", "native"], default="native",
-                    help="BatchNorm2d on channels-last inputs: PyTorch's native NHWC kernels "
-                         "(default) or MIOpen (nets.NATIVE_BN); NCHW always takes MIOpen")
-    ap.add_argument("--bias-grad", choices=["reduce", "gemv"], default="reduce",
-                    help="stride-2 ConvTranspose2d bias gradient: strided reduction or a "
-                         "ones-vector GEMM (nets.BIAS_GEMV)")
-    ap.add_argument("--deconv", choices=["transposed", "phase", "mfma"], default="mfma",
-                    help="stride-2 ConvTranspose2d: MIOpen's transposed convolution, one 3x3 "
-                         "convolution + pixel shuffle (nets.PHASE_DECONV), or the library's MFMA "
-                         "kernel for bf16 channels-last (nets.MFMA_DECONV)")
+    ap.add_argument("--deconv", choices=["transposed", "mfma"], default="mfma",
+                    help="stride-2 ConvTranspose2d: MIOpen's transposed convolution or the "
+                         "library's MFMA kernel for bf16 channels-last (nets.MFMA_DECONV)")
     ap.add_argument("--conv-dgrad", choices=["mfma", "miopen"], default="mfma",
                     help="encoder Conv2d(4, 2, 1) input gradients on the library's transposed-conv "
                          "kernel (nets.MFMA_CONV_DGRAD) or MIOpen")
@@ -112,9 +105,6 @@ def main():
     from lie_vae.experiments.train_dp import DPTrainer, param_count
     from lie_vae.experiments.vae import VAE
     nets.GEMM_LAYERS = args.conv_gemm == "on"
-    nets.NATIVE_BN = args.bn == "native"
-    nets.BIAS_GEMV = args.bias_grad == "gemv"
-    nets.PHASE_DECONV = args.deconv == "phase"
     nets.MFMA_DECONV = args.deconv == "mfma"
     nets.FUSED_RELU = args.fused_relu == "on"
     nets.MFMA_CONV_DGRAD = args.conv_dgrad == "mfma"
@@ -166,7 +156,7 @@ def main():
                        "params": param_count(model),
                        "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
                        "channels_last": args.channels_last, "miopen_find": args.find,
-                       "conv_gemm": args.conv_gemm, "bn": args.bn, "bias_grad": args.bias_grad,
+                       "conv_gemm": args.conv_gemm,
                        "deconv": args.deconv, "fused_relu": args.fused_relu, "conv_dgrad": args.conv_dgrad, "adam": args.adam,
                        "launch": "graph" if args.graph else "eager"},
             "matrix": {"flops_per_step_per_gpu": step_flops,

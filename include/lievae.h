@@ -251,28 +251,16 @@ int lv_bn_lrelu_bwd_bf16(const void* g, const void* x, const float* gamma, const
                          float* ggamma, float* gbeta, float* ws, int64_t P, int C, void* stream);
 /* Fused ReLU around the decoder layers (DeconvNet's nn.ReLU, nets.py:62-72), flags:
  *   LV_DECONV_RELU_OUT  y = max(conv_transpose(x) + b, 0) (the ReLU after the layer);
- *   LV_DECONV_RELU_IN   the layer reads max(x, 0) (the ReLU in front of it): forward and
- *                       wgrad use max(x, 0) and gx is the gradient w.r.t. x itself (masked
- *                       by x > 0).  Small-Cout layer only;
  *   LV_DECONV_MASK_GX   (backward, small-Cout layer) gx masked by x > 0 only: x is already a
  *                       ReLU output (e.g. written with LV_DECONV_RELU_OUT), so forward and
  *                       wgrad need no max and gx is the gradient w.r.t. the ReLU's input. */
 #define LV_DECONV_RELU_OUT 1
-#define LV_DECONV_RELU_IN 2
 #define LV_DECONV_MASK_GX 4
 int lv_deconv4s2_fwd_bf16_ex(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                              int H, int W, int Cin, int Cout, int flags, void* stream);
-int lv_deconv4s2_small_fwd_bf16_ex(const void* x, const void* wq, const float* bias, void* y,
-                                   int64_t N, int H, int W, int Cin, int Cout, int flags, void* stream);
 int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd, void* gx, void* gw,
                                    float* gb, float* ws, int64_t N, int H, int W, int Cin, int Cout,
                                    int flags, void* stream);
-/* Same with an explicit kernel variant (A/B): 0 = the default, 128 / 256 = v1 (register-
- * staged double buffer) with that pixel-tile height, 2 / 3 = v2 (LDS-DMA ring of that many
- * stages, 4 x 2 wave tiling), 4 / 5 = v2 with 2 / 3 stages and XCD-grouped phases, 6 / 7 =
- * the same with 128-row block tiles (2 x 4 waves; 6 is the default). */
-int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y,
-                               int64_t N, int H, int W, int Cin, int Cout, int bm, void* stream);
 
 #ifdef __cplusplus
 }

@@ -32,14 +32,8 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// ReLU of 8 packed bf16 (a 16-byte piece): max(bits, 0) as signed 16-bit integers zeroes
-// every value with the sign bit set (negatives, -0) and keeps the rest -- v_pk_max_i16.
 typedef short s16x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ u32x4 relu_bf16x8(u32x4 v) {
-  const s16x8 t = __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), s16x8(0));
-  return __builtin_bit_cast(u32x4, t);
-}
+
 // g where x > 0 (ReLU backward against its output x), 8 packed bf16: x > 0 <=> the signed
 // 16-bit pattern is positive (a +NaN x also passes; the reference's mask would drop it).
 __device__ __forceinline__ u32x4 relu_mask_bf16x8(u32x4 g, u32x4 x) {
@@ -489,7 +483,6 @@ struct DeconvSmallArgs {
   const float* bias;          // (Cout) or null
   __hip_bfloat16* y;          // (N, 2H, 2W, Cout) bf16 channels-last
   int H, W, Cin, Cout, tiles_w;
-  int relu_in;                // the layer's input passes through ReLU first (x -> max(x, 0))
 };
 
 __global__ __launch_bounds__(kSmallThreads) void deconv_small_kernel(DeconvSmallArgs a) {
@@ -518,7 +511,6 @@ __global__ __launch_bounds__(kSmallThreads) void deconv_small_kernel(DeconvSmall
         const int c = ch * 32 + q * 8;
         if (ia >= 0 && ia < a.H && ib >= 0 && ib < a.W && c < a.Cin) {
           rx[i] = *reinterpret_cast<const u32x4*>(ximg + ((int64_t)ia * a.W + ib) * a.Cin + c);
-          if (a.relu_in) rx[i] = relu_bf16x8(rx[i]);
         }
       }
     }
@@ -622,8 +614,6 @@ struct DeconvSmallBwdArgs {
   int H, W, Cin, Cout, nct, tiles_w;
   int tiles_img;              // tiles per image
   int64_t ntiles;
-  int relu_in;                // x is the input of a ReLU in front of the layer: the layer sees
-                              // max(x, 0) (wgrad); dgrad masks gx by x > 0 (template MASK)
 };
 
 // wd[c][nbr·16 + n] = Wq[nbr, c, n] (0 past Cin, past 4·Cout and for nbr = 9): the dgrad
@@ -694,7 +684,7 @@ __device__ __forceinline__ TileAt tile_at(const DeconvSmallBwdArgs& a, int64_t t
 // 16-byte quad reads (B operand: K = 8 consecutive (nbr, n) of one pixel), five MFMAs per
 // channel tile (C rows = 4 consecutive channels per lane -> one 8-byte LDS store), then the
 // staged [64 pixels][Cin] tile leaves as 16-byte stores of whole pixel rows.
-// MASK: gx is masked by x > 0 (the ReLU in front of the layer, LV_DECONV_RELU_IN /
+// MASK: gx is masked by x > 0 (the ReLU in front of the layer,
 // LV_DECONV_MASK_GX); the tile's x pieces are loaded right after the quad stage, so their
 // latency hides under the tile's MFMAs.
 template <int CO, bool MASK>
@@ -852,7 +842,6 @@ __global__ __launch_bounds__(kWgThreads) void deconv_small_wgrad_kernel(DeconvSm
       if (e < kBwPix * G8 && ia < a.H && ib < a.W) {
         if (c < a.Cin) {
           xv[i] = *reinterpret_cast<const u32x4*>(a.x + ((t.n * a.H + ia) * a.W + ib) * a.Cin + c);
-          if (a.relu_in) xv[i] = relu_bf16x8(xv[i]);
         }
         else if (c == a.Cin)
           xv[i][0] = 0x3f80u;  // bf16 1.0 in element 0 (channel Cin)
@@ -1040,8 +1029,11 @@ int launch_deconv(const DeconvArgs& a, hipStream_t st) {
 }  // namespace
 
 extern "C" {
+#ifdef LV_AB_KNOBS
+// A/B build only (liblievae_hip_ab.so, tools/deconv_bench.py): an explicit kernel variant
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                                int H, int W, int Cin, int Cout, int bm, void* stream);
+#endif
 
 size_t lv_deconv4s2_packed_weight_elems(int Cin) { return 4 * (size_t)kBN * 4 * (size_t)Cin + 32; }
 
@@ -1086,10 +1078,15 @@ static int deconv_fwd(const void* x, const void* wt, const float* bias, void* y,
   if (bm == 7) return launch_deconv_v2<3, true, 128>(a, (hipStream_t)stream);
   return bm == 256 ? launch_deconv<256>(a, (hipStream_t)stream) : launch_deconv<128>(a, (hipStream_t)stream);
 }
+#ifdef LV_AB_KNOBS
+// bm: 0 = the default, 128 / 256 = v1 (register-staged double buffer) with that pixel-tile
+// height, 2 / 3 = v2 (LDS-DMA ring of that many stages, 4 x 2 wave tiling), 4 / 5 = v2 with
+// 2 / 3 stages and XCD-grouped phases, 6 / 7 = the same with 128-row block tiles
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                                int H, int W, int Cin, int Cout, int bm, void* stream) {
   return deconv_fwd(x, wt, bias, y, N, H, W, Cin, Cout, bm, 0, stream);
 }
+#endif
 int lv_deconv4s2_fwd_bf16_ex(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                              int H, int W, int Cin, int Cout, int flags, void* stream) {
   return deconv_fwd(x, wt, bias, y, N, H, W, Cin, Cout, 0, flags, stream);
@@ -1110,12 +1107,7 @@ int lv_deconv4s2_small_pack_weight_bf16(const void* w, void* wq, int Cin, int Co
 
 int lv_deconv4s2_small_fwd_bf16(const void* x, const void* wq, const float* bias, void* y, int64_t N,
                                 int H, int W, int Cin, int Cout, void* stream) {
-  return lv_deconv4s2_small_fwd_bf16_ex(x, wq, bias, y, N, H, W, Cin, Cout, 0, stream);
-}
-int lv_deconv4s2_small_fwd_bf16_ex(const void* x, const void* wq, const float* bias, void* y, int64_t N,
-                                   int H, int W, int Cin, int Cout, int flags, void* stream) {
   clear_error();
-  LV_CHECK_ARG((flags & ~LV_DECONV_RELU_IN) == 0, "flags: only LV_DECONV_RELU_IN for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0, "Cin must be a positive multiple of 8 (got %d)", Cin);
   LV_CHECK_ARG(Cout >= 1 && Cout <= kSmallMaxCout, "Cout must be in [1, %d] (got %d)", kSmallMaxCout, Cout);
@@ -1123,8 +1115,7 @@ int lv_deconv4s2_small_fwd_bf16_ex(const void* x, const void* wq, const float* b
   if (N == 0) return LV_OK;
   LV_CHECK_ARG(x && wq && y, "null pointer");
   const int th = (H + kSqH - 1) / kSqH, tw = (W + kSqW - 1) / kSqW;
-  DeconvSmallArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wq, bias, (__hip_bfloat16*)y, H, W, Cin, Cout, tw,
-                    (flags & LV_DECONV_RELU_IN) ? 1 : 0};
+  DeconvSmallArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wq, bias, (__hip_bfloat16*)y, H, W, Cin, Cout, tw};
   hipLaunchKernelGGL(deconv_small_kernel, dim3(th * tw, (unsigned)N), dim3(kSmallThreads), 0,
                      (hipStream_t)stream, a);
   LV_RETURN_LAUNCH("deconv_small_kernel");
@@ -1179,8 +1170,7 @@ int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd
                                    float* ws, int64_t N, int H, int W, int Cin, int Cout, int flags,
                                    void* stream) {
   clear_error();
-  LV_CHECK_ARG((flags & ~(LV_DECONV_RELU_IN | LV_DECONV_MASK_GX)) == 0,
-               "flags: only LV_DECONV_RELU_IN / LV_DECONV_MASK_GX for this layer");
+  LV_CHECK_ARG((flags & ~LV_DECONV_MASK_GX) == 0, "flags: only LV_DECONV_MASK_GX for this layer");
   LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
   LV_CHECK_ARG(Cin > 0 && Cin % 8 == 0 && small_bwd_nct(Cin) <= kBwMaxCt,
                "Cin must be a positive multiple of 8 below %d (got %d)", 16 * kBwMaxCt, Cin);
@@ -1192,8 +1182,7 @@ int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd
   const int tw = (W + kBwTB - 1) / kBwTB, th = (H + kBwTA - 1) / kBwTA;
   const int64_t ntiles = N * th * tw;
   DeconvSmallBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)gy, (const __hip_bfloat16*)wd,
-                       (__hip_bfloat16*)gx, ws, H, W, Cin, Cout, small_bwd_nct(Cin), tw, th * tw, ntiles,
-                       (flags & LV_DECONV_RELU_IN) ? 1 : 0};
+                       (__hip_bfloat16*)gx, ws, H, W, Cin, Cout, small_bwd_nct(Cin), tw, th * tw, ntiles};
   const int nw = Cin * Cout * 16;
   if (ntiles == 0) {  // empty batch: zero gradients
     if (gw) LV_CHECK_HIP(hipMemsetAsync(gw, 0, (size_t)nw * 2, st));
@@ -1202,7 +1191,7 @@ int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd
   }
   if (gx) {
     const size_t lds = ((size_t)(kBwQuads + 1) * 16 + (size_t)kBwPix * (a.nct * 16 + 8)) * 2;
-    const bool mask = (flags & (LV_DECONV_RELU_IN | LV_DECONV_MASK_GX)) != 0;
+    const bool mask = (flags & LV_DECONV_MASK_GX) != 0;
     auto k = mask ? (Cout == 1 ? deconv_small_dgrad_kernel<1, true> : Cout == 2 ? deconv_small_dgrad_kernel<2, true>
                      : Cout == 3 ? deconv_small_dgrad_kernel<3, true> : deconv_small_dgrad_kernel<4, true>)
                   : (Cout == 1 ? deconv_small_dgrad_kernel<1, false> : Cout == 2 ? deconv_small_dgrad_kernel<2, false>

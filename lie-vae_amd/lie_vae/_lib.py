@@ -67,15 +67,13 @@ for _name in ("lv_so3_exp_fwd", "lv_so3_exp_bwd", "lv_so3_sample_fwd", "lv_so3_s
     _SIGS[_name + "_f64"] = _SIGS[_name]
 _SIGS["lv_deconv4s2_pack_weight_bf16"] = [_P, _P, _I, _I, _P]
 _SIGS["lv_deconv4s2_fwd_bf16"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _P]
-_SIGS["lv_deconv4s2_fwd_bf16_tile"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_pack_weight_bf16"] = [_P, _P, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_fwd_bf16"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_pack_dgrad_weight_bf16"] = [_P, _P, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_fwd_bf16_ex"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
-_SIGS["lv_deconv4s2_small_fwd_bf16_ex"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_bwd_bf16_ex"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
-LV_DECONV_RELU_OUT, LV_DECONV_RELU_IN, LV_DECONV_MASK_GX = 1, 2, 4  # include/lievae.h
+LV_DECONV_RELU_OUT, LV_DECONV_MASK_GX = 1, 4  # include/lievae.h
 _SIGS["lv_channel_sum_bf16"] = [_P, _P, _P, _I64, _I, _P]
 _SIGS["lv_bn_lrelu_fwd_bf16"] = [_P, _P, _P, _P, _P, _I, _F, _F, _F, _P, _P, _P, _P, _I64, _I, _P]
 _SIGS["lv_bn_lrelu_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I64, _I, _P]
@@ -91,6 +89,9 @@ _SIGS_EXTRA = {"lv_group_action_bwd_workspace": [_I64, _I, _I, _I], "lv_last_err
                "lv_bn_supported": [_I64, _I], "lv_bn_workspace_elems": [_I64, _I]}
 
 EXPORTED = sorted(list(_SIGS) + list(_SIGS_EXTRA))
+# entry points of the A/B build only (liblievae_hip_ab.so, -DLV_AB_KNOBS; tools/ sweeps):
+# bound when the loaded library has them, never part of the product header
+_SIGS_AB = {"lv_deconv4s2_fwd_bf16_tile": [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]}
 
 _lib = None
 
@@ -113,6 +114,9 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    for name, args in _SIGS_AB.items():
+        if hasattr(lib, name):
+            getattr(lib, name).argtypes = args
     _lib = lib
     return lib
 

@@ -201,6 +201,29 @@ class _SO3LogPosterior(torch.autograd.Function):
 
 
 # ------------------------------------------------------------ group action
+_WS_BYTES = {}   # (n, L, C, shared F) -> lv_group_action_bwd_workspace
+_WS_BUF = {}     # (device index, raw stream) -> cached uint8 workspace (eager calls only)
+
+
+def _bwd_workspace(n, L, C, shared, device):
+    """The backward's workspace: its size queried once per shape, the buffer reused per
+    (device, stream) for eager calls (stream order serialises its users).  Under graph
+    capture a fresh allocation from the graph's pool keeps replays independent of eager
+    calls on other streams."""
+    key = (n, L, C, shared)
+    nb = _WS_BYTES.get(key)
+    if nb is None:
+        nb = _WS_BYTES[key] = int(_lib.load().lv_group_action_bwd_workspace(n, L, C, shared))
+    st = stream()
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(max(nb, 1), device=device, dtype=torch.uint8), nb, st
+    bkey = (device.index, st)
+    buf = _WS_BUF.get(bkey)
+    if buf is None or buf.numel() < nb:
+        buf = _WS_BUF[bkey] = torch.empty(max(nb, 1 << 20), device=device, dtype=torch.uint8)
+    return buf, nb, st
+
+
 class _GroupAction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, angles, spec, L, transpose, out_dtype):
@@ -224,10 +247,9 @@ class _GroupAction(torch.autograd.Function):
         gout = _prep(gout)
         gang = torch.empty_like(angles)
         gspec = torch.empty_like(spec)
-        ws_bytes = _lib.load().lv_group_action_bwd_workspace(n, L, C, int(ctx.stride == 0))
-        ws = torch.empty(max(ws_bytes, 1), device=angles.device, dtype=torch.uint8)
+        ws, ws_bytes, st = _bwd_workspace(n, L, C, int(ctx.stride == 0), angles.device)
         call("lv_group_action_bwd", ptr(angles), ptr(spec), ctx.stride, ptr(gout), ptr(gang),
-             ptr(gspec), n, L, C, int(ctx.transpose), ptr(ws), ws_bytes, stream())
+             ptr(gspec), n, L, C, int(ctx.transpose), ws.data_ptr(), ws_bytes, st)
         return gang, gspec, None, None, None
 
 
@@ -281,7 +303,7 @@ class _FusedExpAction(torch.autograd.Function):
         ang = _empty((n, 3), v)
         call("lv_fused_exp_action_fwd", ptr(mu_c), ptr(v), ptr(spec), stride, ptr(out), dt,
              ptr(ang), n, L, C, int(transpose), stream())
-        ctx.save_for_backward(mu_c if mu_c is not None else v.new_empty(0), v, spec, ang)
+        ctx.save_for_backward(mu_c, v, spec, ang)
         ctx.has_mu, ctx.L, ctx.transpose, ctx.stride = mu is not None, L, transpose, stride
         return out
 
@@ -291,13 +313,12 @@ class _FusedExpAction(torch.autograd.Function):
         n, L, C = v.shape[0], ctx.L, spec.shape[-1]
         gout = _prep(gout)
         gspec = torch.empty_like(spec)
-        ws_bytes = _lib.load().lv_group_action_bwd_workspace(n, L, C, 1)
-        ws = torch.empty(max(ws_bytes, 1), device=v.device, dtype=torch.uint8)
+        ws, ws_bytes, st = _bwd_workspace(n, L, C, 1, v.device)
         gv = torch.empty_like(v)
         gmu = torch.empty_like(mu) if ctx.has_mu else None
-        call("lv_fused_exp_action_bwd", ptr(mu) if ctx.has_mu else None, ptr(v), ptr(ang),
-             ptr(spec), ptr(gout), ptr(gmu), ptr(gv), ptr(gspec), n, L, C, int(ctx.transpose),
-             ptr(ws), ws_bytes, stream())
+        call("lv_fused_exp_action_bwd", ptr(mu), v.data_ptr(), ang.data_ptr(), spec.data_ptr(),
+             gout.data_ptr(), ptr(gmu), gv.data_ptr(), gspec.data_ptr(), n, L, C,
+             int(ctx.transpose), ws.data_ptr(), ws_bytes, st)
         return gmu, gv, gspec, None, None, None
 
 

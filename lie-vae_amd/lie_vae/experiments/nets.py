@@ -76,35 +76,10 @@ class GemmConv2d(nn.Conv2d):
         return y.view(B, self.out_channels, 1, 1)
 
 
-# Switches for the memory-bound pieces of the conv stacks (bench_train.py --bn /
-# --bias-grad / --deconv; read when a model is built).  Measured on MI355X, config 3
-# (B = 512, steady state, profiles/r03_train_ab.txt):
-#   NATIVE_BN: BatchNorm2d on channels-last inputs through PyTorch's native NHWC kernels
-#              instead of MIOpen's (bf16 NHWC step 7.66 -> 7.41 ms); NCHW inputs keep
-#              MIOpen, which is faster there (f32 NCHW 14.2 vs 15.2 ms with native)
-#   BIAS_GEMV: the stride-2 ConvTranspose2d bias gradient as a ones-vector GEMM (off:
-#              10.0 vs 7.7 ms -- without its bias MIOpen picks slower deconv solutions)
-NATIVE_BN = True
-BIAS_GEMV = False
 # FUSED_BN_ACT: the encoder's BatchNorm2d + LeakyReLU pair as FusedBatchNormLeakyReLU (the
 # library's deterministic bf16 channels-last kernels, csrc/bn.hip) + an Identity placeholder
 # (same Sequential indices and state_dict keys).
 FUSED_BN_ACT = True
-
-
-class NativeBatchNorm2d(nn.BatchNorm2d):
-    """BatchNorm2d evaluated by PyTorch's native kernels for channels-last inputs (MIOpen
-    disabled for this op only); same parameters, buffers and arithmetic definition."""
-
-    def forward(self, x):
-        if not _cl(x):
-            return super().forward(x)
-        prev = torch.backends.cudnn.enabled
-        torch.backends.cudnn.enabled = False
-        try:
-            return super().forward(x)
-        finally:
-            torch.backends.cudnn.enabled = prev
 
 
 class _BnLeakyReLU(torch.autograd.Function):
@@ -162,6 +137,12 @@ class FusedBatchNormLeakyReLU(nn.BatchNorm2d):
         if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and _cl(x)
                 and self.training and self.track_running_stats and self.momentum is not None):
             return False
+        # the kernels read gamma / beta / running stats as float* and write fp32 gamma /
+        # beta gradients into buffers shaped like the parameters, and load x in 16-byte
+        # pieces: a bf16 model (model.to(bfloat16)) or a misaligned view takes the fallback
+        if x.data_ptr() % 16 or any(t is not None and (t.dtype != torch.float32 or not t.is_contiguous())
+                                    for t in (self.weight, self.bias, self.running_mean, self.running_var)):
+            return False
         N, C, H, W = x.shape
         return N * H * W > 1 and bool(_lib.load().lv_bn_supported(N * H * W, C))
 
@@ -209,46 +190,13 @@ def to_sync_batchnorm(module, process_group=None):
     return module
 
 
-class _BiasAdd(torch.autograd.Function):
-    """y + b[c] with the bias gradient sum_{n,h,w} g[n, c, h, w] as ones[1, NHW] @ G[NHW, C]
-    when G is channels-last (a GEMM on hipBLASLt), else a plain sum."""
-
-    @staticmethod
-    def forward(ctx, y, b):
-        ctx.bdt = b.dtype
-        return y + b.to(y.dtype).view(1, -1, 1, 1)
-
-    @staticmethod
-    def backward(ctx, g):
-        C = g.shape[1]
-        if _cl(g):
-            g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
-            ones = g2.new_ones(1, g2.shape[0])
-            gb = (ones @ g2).view(C)
-        else:
-            gb = g.sum((0, 2, 3))
-        return g, gb.to(ctx.bdt)
-
-
-class BiasGemvConvTranspose2d(nn.ConvTranspose2d):
-    """ConvTranspose2d whose bias is added by _BiasAdd (same parameters / state_dict)."""
-
-    def forward(self, x, output_size=None):
-        if self.bias is None or output_size is not None:
-            return super().forward(x, output_size)
-        y = torch.nn.functional.conv_transpose2d(x, self.weight, None, self.stride, self.padding,
-                                                 self.output_padding, self.groups, self.dilation)
-        return _BiasAdd.apply(y, self.bias)
-
-
-PHASE_DECONV = False  # off: 10.5 vs 7.4 ms (bf16), 22.1 vs 15.2 ms (f32)
 # The stride-2 ConvTranspose2d forward on the library's MFMA kernels (lv_deconv4s2_fwd_bf16
 # and, for the RGB output layer, lv_deconv4s2_small_fwd_bf16; csrc/deconv.hip) when it runs
 # in bf16 (autocast) on channels-last inputs; fp32 / NCHW / unsupported shapes keep MIOpen.
 # Config 3 bf16: 7.41 -> 6.29 ms/step (dec5 forward 989 -> 77 us, dec2-4 2x faster).
 MFMA_DECONV = True
 # DeconvNet's ReLUs fused into the neighbouring MFMA layers (MfmaConvTranspose2d.relu_out /
-# relu_in): the forward clamps and the largest ReLU backward (after the 4th layer, folded
+# input_is_relu): the forward clamps and the largest ReLU backward (after the 4th layer, folded
 # into the RGB layer's dgrad epilogue) leave the step.
 FUSED_RELU = True
 
@@ -276,11 +224,9 @@ class _Deconv4s2(torch.autograd.Function):
     flags (include/lievae.h): LV_DECONV_RELU_OUT (Cout > 4) returns relu(y) from the
     forward epilogue, and the backward masks gy by y > 0 (ReLU's backward against its
     output) before the layer's own -- unless SKIP_MASK says the consumer of y already
-    returns a masked gradient; LV_DECONV_RELU_IN (Cout <= 4) makes the layer read relu(x):
-    forward and wgrad stage max(x, 0), and dgrad's epilogue masks gx by x > 0, so the
-    returned gx is the gradient w.r.t. the ReLU's input; LV_DECONV_MASK_GX (Cout <= 4) is
-    the dgrad mask alone, for an x that is already a ReLU output.  All reproduce the
-    unfused nn.ReLU + layer bit for bit."""
+    returns a masked gradient; LV_DECONV_MASK_GX (Cout <= 4) masks the dgrad output by
+    x > 0, for an x that is a ReLU output (the ReLU's backward in the layer's epilogue).
+    Both reproduce the unfused nn.ReLU + layer bit for bit."""
 
     SKIP_MASK = 1 << 8  # python-side flag, never passed to the library
 
@@ -291,8 +237,7 @@ class _Deconv4s2(torch.autograd.Function):
         Cout = w.shape[1]
         wc = w.contiguous()
         small = Cout <= 4  # the RGB output layer: quad GEMM over the 3x3 neighbourhood
-        ok = ((_lib.LV_DECONV_RELU_IN | _lib.LV_DECONV_MASK_GX) if small
-              else (_lib.LV_DECONV_RELU_OUT | _Deconv4s2.SKIP_MASK))
+        ok = _lib.LV_DECONV_MASK_GX if small else (_lib.LV_DECONV_RELU_OUT | _Deconv4s2.SKIP_MASK)
         assert flags & ~ok == 0, f"flags {flags} not supported for Cout={Cout}"
         pre = "lv_deconv4s2_small_" if small else "lv_deconv4s2_"
         wt = torch.empty(getattr(_lib.load(), pre + "packed_weight_elems")(Cin), device=x.device,
@@ -301,13 +246,17 @@ class _Deconv4s2(torch.autograd.Function):
                         memory_format=torch.channels_last)
         st = _lib.stream()
         _lib.call(pre + "pack_weight_bf16", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
-        _lib.call(pre + "fwd_bf16_ex", x.data_ptr(), wt.data_ptr(),
-                  None if b is None else b.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout,
-                  flags & (_lib.LV_DECONV_RELU_IN | _lib.LV_DECONV_RELU_OUT), st)
+        args = (x.data_ptr(), wt.data_ptr(), None if b is None else b.data_ptr(), y.data_ptr(),
+                N, H, W, Cin, Cout)
+        if small:
+            _lib.call("lv_deconv4s2_small_fwd_bf16", *args, st)
+        else:
+            _lib.call("lv_deconv4s2_fwd_bf16_ex", *args, flags & _lib.LV_DECONV_RELU_OUT, st)
         relu_out = bool(flags & _lib.LV_DECONV_RELU_OUT) and not flags & _Deconv4s2.SKIP_MASK
         ctx.save_for_backward(x, wc, *((y,) if relu_out else ()))
         ctx.has_bias = b is not None
         ctx.flags = flags
+        ctx.w_cl = _cl(w)  # the gradient comes back in the parameter's memory format
         return y
 
     @staticmethod
@@ -339,44 +288,43 @@ class _Deconv4s2(torch.autograd.Function):
                       None if wd is None else wd.data_ptr(), None if gx is None else gx.data_ptr(),
                       None if gw is None else gw.data_ptr(), None if gb is None else gb.data_ptr(),
                       None if ws is None else ws.data_ptr(), N, H, W, Cin, Cout, ctx.flags, st)
-            return gx, (_like(gw, w) if need_w else None), gb, None
+            return gx, (_like(gw, ctx.w_cl) if need_w else None), gb, None
         gx, gw, _ = torch.ops.aten.convolution_backward(
             gy, x, w, None, [2, 2], [1, 1], [1, 1], True, [0, 0], 1, [need_x, need_w, False])
-        return gx, _like(gw, w), (_channel_sum(gy) if need_b else None), None
+        return gx, _like(gw, ctx.w_cl), (_channel_sum(gy) if need_b else None), None
 
 
-def _like(g, w):
+def _like(g, channels_last):
     """A weight gradient in its parameter's memory format (a channels-last model keeps
-    channels-last weights): AccumulateGrad then stores it as is, and the optimizer sees
-    params and grads of one layout -- the condition for torch.optim's foreach / fused
-    Adam paths (otherwise Adam falls back to one chain of kernels per tensor)."""
-    if g is None or g.stride() == w.stride():
+    channels-last weights; ``channels_last`` is _cl of the parameter as the layer received
+    it): AccumulateGrad then stores it as is, and the optimizer sees params and grads of
+    one layout -- the condition for torch.optim's foreach / fused Adam paths (otherwise
+    Adam falls back to one chain of kernels per tensor)."""
+    if g is None:
         return g
-    return g.contiguous(memory_format=torch.channels_last) if w.is_contiguous(
-        memory_format=torch.channels_last) else g.contiguous()
+    return g.contiguous(memory_format=torch.channels_last) if channels_last else g.contiguous()
 
 
 class MfmaConvTranspose2d(nn.ConvTranspose2d):
     """nn.ConvTranspose2d (same parameters / state_dict) whose k4 s2 p1 forward runs on
     the MFMA kernel for bf16 channels-last inputs (autocast bf16, or bf16 tensors).
 
-    relu_in / relu_out (plain attributes, not state): the layer computes
-    layer(relu(x)) / relu(layer(x)) -- DeconvNet moves its nn.ReLU modules into the
-    neighbouring layers this way (FUSED_RELU); the MFMA path fuses relu_out for Cout > 4
-    and relu_in for Cout <= 4 into the kernels, everything else applies F.relu.
+    relu_out (a plain attribute, not state): the layer computes relu(layer(x)) --
+    DeconvNet moves its nn.ReLU modules into the neighbouring layers this way
+    (FUSED_RELU); the MFMA path fuses it for Cout > 4 into the kernel's epilogue,
+    everything else applies F.relu.
     input_is_relu: x is a ReLU output (relu(x) = x), so only the ReLU's backward mask
     remains, in the RGB layer's dgrad epilogue; grad_masked_downstream (on the layer that
     produced that x with relu_out): its consumer returns the masked gradient, so its own
     backward skips the mask.  Either way the consumer's fallback path applies F.relu,
     whose backward masks."""
 
-    relu_in = False
     relu_out = False
     input_is_relu = False
     grad_masked_downstream = False
 
     def extra_repr(self):
-        fl = [n for n in ("relu_in", "relu_out", "input_is_relu", "grad_masked_downstream") if getattr(self, n)]
+        fl = [n for n in ("relu_out", "input_is_relu", "grad_masked_downstream") if getattr(self, n)]
         return super().extra_repr() + "".join(f", {n}=True" for n in fl)
 
     def _mfma_ok(self, x):
@@ -385,24 +333,26 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
                 and self.output_padding == (0, 0) and self.dilation == (1, 1)
                 and self.groups == 1 and self.in_channels % 8 == 0
                 and ((self.out_channels % 8 == 0 and self.out_channels <= 208)
-                     or self.out_channels <= 4) and x.shape[0] <= 65535)
+                     # the small-Cout backward holds Cin + 1 (bias) channels in <= 16
+                     # 16-wide tiles (lv_deconv4s2_small_bwd_bf16: kBwMaxCt)
+                     or (self.out_channels <= 4 and self.in_channels <= 248))
+                and x.shape[0] <= 65535)
 
     def forward(self, x, output_size=None):
         F_ = torch.nn.functional
         bf16 = x.dtype == torch.bfloat16 or (
             torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
         if output_size is not None or not bf16 or not self._mfma_ok(x):
-            y = super().forward(F_.relu(x) if self.relu_in or self.input_is_relu else x, output_size)
+            y = super().forward(F_.relu(x) if self.input_is_relu else x, output_size)
             return F_.relu(y) if self.relu_out else y
         from .. import _lib
         small = self.out_channels <= 4
-        flags = ((_lib.LV_DECONV_RELU_IN if self.relu_in and small else 0)
-                 | (_lib.LV_DECONV_MASK_GX if self.input_is_relu and not self.relu_in and small else 0)
+        flags = ((_lib.LV_DECONV_MASK_GX if self.input_is_relu and small else 0)
                  | (_lib.LV_DECONV_RELU_OUT if self.relu_out and not small else 0)
                  | (_Deconv4s2.SKIP_MASK if self.relu_out and self.grad_masked_downstream and not small else 0))
         with torch.autocast("cuda", enabled=False):
             xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            if (self.relu_in or self.input_is_relu) and not small:
+            if self.input_is_relu and not small:
                 xb = F_.relu(xb)
             y = _Deconv4s2.apply(xb, self.weight.to(torch.bfloat16),
                                  None if self.bias is None else self.bias.float(), flags)
@@ -427,6 +377,7 @@ class _Conv4s2(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.w_cl = _cl(w)
         return torch.nn.functional.conv2d(x, w, b, 2, 1)
 
     @staticmethod
@@ -451,7 +402,7 @@ class _Conv4s2(torch.autograd.Function):
             _, gw, gb = torch.ops.aten.convolution_backward(
                 gy, x, w, [co] if need_b else None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
                 [False, need_w, need_b])
-        return gx, _like(gw, w), gb
+        return gx, _like(gw, ctx.w_cl), gb
 
 
 class MfmaDgradConv2d(nn.Conv2d):
@@ -478,47 +429,6 @@ class MfmaDgradConv2d(nn.Conv2d):
                                   None if self.bias is None else self.bias.to(torch.bfloat16))
 
 
-class PhaseConvTranspose2d(nn.ConvTranspose2d):
-    """ConvTranspose2d(c_in, c_out, 4, 2, 1) as ONE stride-1 3x3 convolution to 4·c_out
-    channels followed by a pixel shuffle (sub-pixel decomposition): output pixel
-    (2a + r, 2b + s) only sees inputs (a + di, b + dj), di in {r - 1, r}, through kernel tap
-    (3 - 2i + r, 3 - 2j + s) with i = di + 1, so phase (r, s) is a 2x2 sub-kernel of a
-    3x3 window.  The four phases become one forward convolution (an implicit GEMM that
-    MIOpen runs on MFMA) instead of a transposed (backward-data) convolution; the zero
-    taps cost 9/4 of the FLOPs.  Same parameters / state_dict; other shapes fall back."""
-
-    _IDX = {}
-
-    def _phase_ok(self):
-        return (self.kernel_size == (4, 4) and self.stride == (2, 2) and self.padding == (1, 1)
-                and self.output_padding == (0, 0) and self.dilation == (1, 1) and self.groups == 1)
-
-    def _w3(self):
-        dev = self.weight.device
-        if dev not in self._IDX:
-            k = torch.full((2, 3), 4, dtype=torch.long)
-            for r in range(2):
-                for i in range(3):
-                    if i - r in (0, 1):
-                        k[r, i] = 3 - 2 * i + r
-            self._IDX[dev] = k.to(dev)
-        k = self._IDX[dev]
-        w = torch.nn.functional.pad(self.weight, (0, 1, 0, 1))            # (cin, cout, 5, 5)
-        w = w[:, :, k[:, None, :, None], k[None, :, None, :]]            # (cin, cout, r, s, i, j)
-        cin, cout = self.in_channels, self.out_channels
-        return w.permute(1, 2, 3, 0, 4, 5).reshape(4 * cout, cin, 3, 3)
-
-    def forward(self, x, output_size=None):
-        if output_size is not None or not self._phase_ok():
-            return super().forward(x, output_size)
-        w3 = self._w3()
-        if _cl(self.weight):
-            w3 = w3.contiguous(memory_format=torch.channels_last)
-        b3 = self.bias.repeat_interleave(4) if self.bias is not None else None
-        y = torch.nn.functional.conv2d(x, w3, b3, 1, 1)
-        return torch.nn.functional.pixel_shuffle(y, 2)
-
-
 def _conv(*a):
     return (GemmConv2d if GEMM_LAYERS else nn.Conv2d)(*a)
 
@@ -528,15 +438,7 @@ def _convt(*a):
 
 
 def _convt_s2(*a):
-    if MFMA_DECONV:
-        return MfmaConvTranspose2d(*a)
-    if PHASE_DECONV:
-        return PhaseConvTranspose2d(*a)
-    return (BiasGemvConvTranspose2d if BIAS_GEMV else nn.ConvTranspose2d)(*a)
-
-
-def _bn(c):
-    return (NativeBatchNorm2d if NATIVE_BN else nn.BatchNorm2d)(c)
+    return (MfmaConvTranspose2d if MFMA_DECONV else nn.ConvTranspose2d)(*a)
 
 
 class View(nn.Module):
@@ -562,7 +464,7 @@ def _down_stack(in_dims, hidden, out_dims, batch_norm):
             layers += [FusedBatchNormLeakyReLU(width, 0.2), nn.Identity()]
         else:
             if batch_norm:
-                layers.append(_bn(width))
+                layers.append(nn.BatchNorm2d(width))
             layers.append(nn.LeakyReLU(0.2, inplace=True))
         c = width
     layers += [_conv(c, out_dims, 4, 1, 0), Flatten()]

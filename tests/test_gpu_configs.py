@@ -296,6 +296,134 @@ def test_dp_trainer_bf16_autocast_step(gpu_device):
     assert out[torch.bfloat16][0] == pytest.approx(out[None][0], rel=2e-2)
 
 
+# Config-3 benchmarked step (bench_train.py --amp bf16 --channels-last) against the fp32 step.
+# bf16 bound: one bf16 rounding has unit roundoff u = 2^-9.  Along the longest path of a
+# conv/BN parameter's gradient the bf16 step rounds about k = 80 times (each of the 9
+# conv / deconv layers rounds its input, weight and output forward, and its upstream
+# gradient, input and weight gradient backward; the 4 BN+LeakyReLU layers their output and
+# input gradient; the 2 mean / sigma linears likewise).  Independent roundings give a
+# normwise relative error near sqrt(k)·u = 1.7e-2, the first-order worst case is k·u = 0.16;
+# BN's mean subtraction can amplify either.  The test asserts BF16_STEP_TOL = 0.06 on every
+# conv / BN / linear group (between the two, measured values in the docstring) and, on the
+# update Adam applies (sign-like at step 1: lr·g/(|g| + eps)), a cosine >= 0.98.
+BF16_STEP_TOL = 0.06
+
+
+def _param_groups(model):
+    groups = {"encoder": [], "rep_group": [], "item_rep": [], "deconv": []}
+    for name, p in model.named_parameters():
+        if name.startswith("encoder."):
+            groups["encoder"].append(name)
+        elif name.startswith("rep_group."):
+            groups["rep_group"].append(name)
+        elif name == "decoder.item_rep":
+            groups["item_rep"].append(name)
+        else:
+            assert name.startswith("decoder.deconv."), name
+            groups["deconv"].append(name)
+    return groups
+
+
+def test_config3_bf16_step_matches_fp32_step(gpu_device, monkeypatch):
+    """The benchmarked config-3 step end to end at its size (B = 512): one DPTrainer step
+    with amp_dtype=bf16 on a channels-last model with every default fused kernel (MFMA
+    deconv forward, small-layer backward, encoder dgrad, fused BN + LeakyReLU, fused
+    ReLU) against the fp32 step from the same initial state on the same x and eps
+    (reference step: unsupervised.py:108-117 -- loss mean, backward, global-norm clip
+    1e-5, Adam lr 1e-3).
+
+    (a) bf16 step vs fp32 step: loss within 1e-2; per parameter group (encoder convs + BN,
+        mean / sigma linears, item_rep, deconv stack) the clipped gradients within
+        BF16_STEP_TOL normwise (the bf16 bound derived above); the Adam update of every
+        group points the same way (cosine >= 0.98) and the updated parameters agree.
+    (b) Inside the bf16 step the SO(3) kernels still compute in fp32: the fused
+        exp -> ZYZ -> action launch's output and its gradients (item_rep, v, mu), given the
+        step's own inputs and upstream gradient, match the oracle's autograd at fp32 noise
+        (1e-5 output per sample with the 2x rule; 1e-4 gradients normwise)."""
+    import lie_vae._ops as ops
+    from lie_vae.experiments.train_dp import DPTrainer
+    from lie_vae.experiments.vae import VAE
+    from oracle import lie_ref
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
+    L, B = 10, 512
+    torch.manual_seed(0)
+    base = VAE(latent_mode="so3", decoder_mode="action", degrees=L, rep_copies=10, rgb=True,
+               batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(gpu_device)
+    base = base.to(memory_format=torch.channels_last)
+    groups = _param_groups(base)
+    g = torch.Generator().manual_seed(21)
+    x = torch.rand(B, 3, 64, 64, generator=g).to(gpu_device)
+    eps = torch.randn(1, B, 3, generator=g).to(gpu_device)
+    p0 = {k: p.detach().clone() for k, p in base.named_parameters()}
+    orig = ops.fused_exp_action
+    runs = {}
+    for tag, amp in (("f32", None), ("bf16", torch.bfloat16)):
+        m = copy.deepcopy(base)
+        cap = {}
+
+        def wrap(mu, v, spec, L_, transpose=False, out_dtype=torch.float32, cap=cap):
+            out = orig(mu, v, spec, L_, transpose, out_dtype)
+            cap["in"] = (mu.detach().clone(), v.detach().clone(), spec.detach().clone())
+            cap["out"] = out.detach().clone()
+            mu.register_hook(lambda gr: cap.__setitem__("gmu", gr.detach().clone()))
+            v.register_hook(lambda gr: cap.__setitem__("gv", gr.detach().clone()))
+            out.register_hook(lambda gr: cap.__setitem__("gout", gr.detach().clone()))
+            return out
+        monkeypatch.setattr(ops, "fused_exp_action", wrap)
+        m.decoder.item_rep.register_hook(lambda gr, cap=cap: cap.__setitem__("gF", gr.detach().clone()))
+        tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5, amp_dtype=amp)
+        loss, _, _ = tr.step(x, eps)
+        torch.cuda.synchronize()
+        monkeypatch.setattr(ops, "fused_exp_action", orig)
+        assert torch.isfinite(loss)
+        named = dict(m.named_parameters())
+        runs[tag] = {"loss": float(loss), "cap": cap,
+                     "grad": {k: p.grad.detach().float().clone() for k, p in named.items()},
+                     "p": {k: p.detach().clone() for k, p in named.items()}}
+        del m, tr
+    f, b = runs["f32"], runs["bf16"]
+    report = {"loss": abs(b["loss"] - f["loss"]) / abs(f["loss"])}
+
+    def cat(d, names):
+        return torch.cat([d[n].flatten() for n in names]).double()
+    for gname, names in groups.items():
+        gf, gb = cat(f["grad"], names), cat(b["grad"], names)
+        df = cat(f["p"], names) - cat(p0, names)
+        db = cat(b["p"], names) - cat(p0, names)
+        report[gname] = {"grad": float((gb - gf).norm() / gf.norm()),
+                         "update_cos": float((df @ db) / (df.norm() * db.norm())),
+                         "param": float((cat(b["p"], names) - cat(f["p"], names)).norm()
+                                        / cat(f["p"], names).norm())}
+    print("config3 bf16 vs f32 step:", report)
+    assert report["loss"] <= 1e-2, report
+    for gname in groups:
+        r = report[gname]
+        assert r["grad"] <= BF16_STEP_TOL, (gname, report)
+        assert r["update_cos"] >= 0.98, (gname, report)
+        assert r["param"] <= 1e-3, (gname, report)
+    # (b) the fused SO(3) launch inside the bf16 step against the oracle on its own inputs
+    cap = b["cap"]
+    mu, v, F = (t.cpu() for t in cap["in"])
+    gout = cap["gout"].cpu()
+    n = v.shape[0]
+
+    def oracle(dt, grad):
+        ts = [t.to(dt).requires_grad_(grad) for t in (mu, v, F)]
+        y = lie_ref.block_wigner_apply(lie_ref.mat_to_eazyz(lie_ref.so3_sample(ts[0], ts[1])),
+                                       ts[2].expand(n, -1, -1), L)
+        if grad:
+            (y * gout.to(dt)).sum().backward()
+        return y.detach(), [t.grad for t in ts]
+    y32, _ = oracle(torch.float32, False)
+    y64, (gmu64, gv64, gF64) = oracle(torch.float64, True)
+    assert_parity_fp64(host(cap["out"]).reshape(n, -1), y32.numpy().reshape(n, -1),
+                       y64.numpy().reshape(n, -1), what="bf16 step: fused SO(3) forward")
+    for name, got, ref in (("gF", cap["gF"], gF64), ("gv", cap["gv"], gv64), ("gmu", cap["gmu"], gmu64)):
+        assert_normwise(host(got).reshape(1, -1), ref.numpy().reshape(1, -1), 1e-4,
+                        what=f"bf16 step: fused SO(3) {name}")
+
+
 def test_config3_iwae_n500_vs_oracle(gpu_device):
     """The reference's evaluation (main.py:134-139): IWAE log-likelihood with n = 500 on
     the conv VAE, one image per call.  The SO(3) terms (log q over the 500 samples, the
@@ -625,33 +753,59 @@ def test_mfma_conv_dgrad_matches_autograd(gpu_device, N, Cin, Cout, H, W):
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
 
 
-def test_small_deconv_relu_in_bitwise(gpu_device):
-    """The RGB layer's LV_DECONV_RELU_IN (forward / wgrad stage max(x, 0), dgrad masks gx by
-    x > 0) and LV_DECONV_MASK_GX (the mask alone, on an x that is a ReLU output) against
-    relu(x) through the plain kernels and aten's threshold_backward: bit for bit."""
+def test_small_deconv_mask_gx_bitwise(gpu_device):
+    """The RGB layer's LV_DECONV_MASK_GX (dgrad's epilogue masks gx by x > 0, x being a ReLU
+    output) against the plain kernels followed by aten's threshold_backward: bit for bit."""
     from lie_vae import _lib
     from lie_vae.experiments.nets import _Deconv4s2
     g = torch.Generator().manual_seed(17)
     x = torch.randn(3, 200, 17, 16, generator=g).to(torch.bfloat16).to(gpu_device)
-    x = x.contiguous(memory_format=torch.channels_last)
+    x = torch.relu(x).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(200, 3, 4, 4, generator=g) * 0.05).to(torch.bfloat16).to(gpu_device)
     b = torch.randn(3, generator=g).to(gpu_device)
     gy = torch.randn(3, 3, 34, 32, generator=g).to(torch.bfloat16).to(gpu_device)
     gy = gy.contiguous(memory_format=torch.channels_last)
     res = {}
-    for tag, flags, pre in (("ref", 0, True), ("relu_in", _lib.LV_DECONV_RELU_IN, False),
-                            ("mask", _lib.LV_DECONV_MASK_GX, True)):
-        xi = (torch.relu(x) if pre else x).detach().requires_grad_(True)
+    for tag, flags in (("ref", 0), ("mask", _lib.LV_DECONV_MASK_GX)):
+        xi = x.detach().clone().requires_grad_(True)
         wi, bi = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
         y = _Deconv4s2.apply(xi, wi, bi, flags)
         y.backward(gy)
         gx = xi.grad
         if tag == "ref":
-            gx = torch.ops.aten.threshold_backward(gx, torch.relu(x), 0)
+            gx = torch.ops.aten.threshold_backward(gx, x, 0)
         res[tag] = (y.detach(), gx, wi.grad, bi.grad)
-    for tag in ("relu_in", "mask"):
-        for name, a, r in zip(("y", "gx", "gw", "gb"), res[tag], res["ref"]):
-            assert torch.equal(a, r), f"{tag}: {name}"
+    for name, a, r in zip(("y", "gx", "gw", "gb"), res["mask"], res["ref"]):
+        assert torch.equal(a, r), f"mask: {name}"
+
+
+def test_fused_layers_fall_back_outside_their_contract(gpu_device):
+    """FusedBatchNormLeakyReLU with bf16 parameters (model.to(bfloat16)) or a 16-byte
+    misaligned input takes the BatchNorm2d + leaky_relu fallback (the kernels read fp32
+    gamma / beta / running stats and load x in 16-byte pieces); an RGB deconv layer with
+    Cin = 256 (> the small-Cout backward's 248-channel bound) runs nn.ConvTranspose2d
+    instead of failing in backward."""
+    from lie_vae.experiments.nets import FusedBatchNormLeakyReLU, MfmaConvTranspose2d
+    m = FusedBatchNormLeakyReLU(64, 0.2).to(gpu_device)
+    x = torch.randn(8, 64, 8, 8, device=gpu_device).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    assert m._fused_ok(x)
+    assert not copy.deepcopy(m).to(torch.bfloat16)._fused_ok(x)
+    buf = torch.empty(8 * 64 * 8 * 8 + 8, device=gpu_device, dtype=torch.bfloat16)
+    xm = buf[1:1 + x.numel()].view(8, 8, 8, 64).permute(0, 3, 1, 2)  # channels-last, +2 bytes
+    assert xm.data_ptr() % 16 and not m._fused_ok(xm)
+    mb = copy.deepcopy(m).to(torch.bfloat16)
+    y = mb(x.requires_grad_(True))
+    y.float().sum().backward()
+    assert torch.isfinite(x.grad.float()).all() and mb.weight.grad.dtype == torch.bfloat16
+    big = MfmaConvTranspose2d(256, 3, 4, 2, 1).to(gpu_device).to(memory_format=torch.channels_last)
+    xb = torch.randn(2, 256, 8, 8, device=gpu_device).contiguous(memory_format=torch.channels_last)
+    assert not big._mfma_ok(xb)
+    xb.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = big(xb)
+    yb.float().sum().backward()
+    assert torch.isfinite(xb.grad).all() and big.weight.grad is not None
 
 
 def test_fused_relu_deconvnet_bitwise(gpu_device, monkeypatch):

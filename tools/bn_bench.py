@@ -1,14 +1,26 @@
 """Encoder BatchNorm2d + LeakyReLU(0.2), training mode, bf16 channels-last, config-3 shapes
-(batch 512): PyTorch's native NHWC BatchNorm (nets.NativeBatchNorm2d) + leaky_relu vs the
+(batch 512): PyTorch's native NHWC BatchNorm (NativeBatchNorm2d below) + leaky_relu vs the
 library's fused kernels (nets.FusedBatchNormLeakyReLU), forward and forward+backward, HIP
 events over 30 calls.  HBM floor: fwd 3 passes, fwd+bwd 8 passes of the 2·P·C-byte tensor."""
 import json
 import sys
 import torch
 sys.path[:0] = ["lie-vae_amd", "."]
-from lie_vae.experiments.nets import FusedBatchNormLeakyReLU, NativeBatchNorm2d
+from lie_vae.experiments.nets import FusedBatchNormLeakyReLU
 
 dev = torch.device("cuda:0")
+
+
+class NativeBatchNorm2d(torch.nn.BatchNorm2d):
+    """BatchNorm2d by PyTorch's native NHWC kernels (MIOpen disabled for this op only)."""
+
+    def forward(self, x):
+        prev = torch.backends.cudnn.enabled
+        torch.backends.cudnn.enabled = False
+        try:
+            return super().forward(x)
+        finally:
+            torch.backends.cudnn.enabled = prev
 
 
 def timeit(fn, n=30):

@@ -1,6 +1,6 @@
 """HBM traffic per launch of the fused action kernel from rocprofv3 --pmc passes.
 
-Usage: python tools/pmc_traffic.py <pmc_root> <out.json>
+Usage: python tools/pmc_traffic.py <pmc_root> <out.json> [label, e.g. "round 4, HEAD abc123"]
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC EA requests).  Per
 MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of the bytes of wide (16 B/lane)
 coalesced streaming reads on gfx950 -- the kernel's reads (12 B/sample of v plus the
@@ -27,5 +27,7 @@ fetch = res.get("FETCH_SIZE_kib_mean", 0.0) * 1024
 write = res.get("WRITE_SIZE_kib_mean", 0.0) * 1024
 res["hbm_bytes_per_launch"] = fetch + write
 res["hbm_bytes_per_launch_fetch_x2"] = 2 * fetch + write
+if len(sys.argv) > 3:
+    res["measured"] = sys.argv[3]
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
