@@ -178,6 +178,7 @@ constexpr double kTileSegCostLarge = 560.0;  // ... many groups (>= kTileManyGro
 constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
+constexpr int kTileBf16Default = 0;  // bf16 tile options in the product (kTileBf16* bits)
 
 // A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
 // LV_*_NSEG force segment counts, LV_BWD_FGLOBAL forces the backward's global-spectrum
@@ -199,9 +200,17 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
   static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
   static const int kEnvPrio = LV_KNOB("LV_TILE_PRIO", 2);      // wave priority phases (ActionArgs)
+  // bf16 tile with compile-time C: kTileBf16* options and the samples per block (A/B knobs
+  // LV_TILE_BF16 = option bits, LV_TILE_SW = samples per block)
+  static const int kEnvBf16 = LV_KNOB("LV_TILE_BF16", kTileBf16Default);
+  static const int kEnvSw = LV_KNOB("LV_TILE_SW", 0);
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
-  const int Sw = 64 / a.C;
+  const bool bt = out_bytes == 2 && a.C == kTileFastC;
+  int Sw = 64 / a.C;
+  a.tflags = bt ? kEnvBf16 : 0;
+  if (bt && kEnvSw >= 2 && kEnvSw < Sw) Sw = kEnvSw;
+  if (Sw < 2) a.tflags &= ~kTileBf16SpecAlias;
   const int64_t groups = (a.n + Sw - 1) / Sw;
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
@@ -218,8 +227,11 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   if (a.C != kTileFastC && L < kTileFGlobalMinL)
     for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
   a.fpitch = (fp + 3) & ~3;
-  // (C = kTileFastC with fp32 output: the spectrum sits in the tile's last sample slot)
-  const size_t fl = a.C == kTileFastC ? (out_bytes == 4 ? 0 : (size_t)a.MC) : (size_t)nseg * a.fpitch;
+  // (C = kTileFastC with fp32 output: the spectrum sits in the tile's last sample slot;
+  // bf16 with kTileBf16SpecAlias: in its last two)
+  const size_t fl = a.C == kTileFastC
+                        ? (out_bytes == 4 || (a.tflags & kTileBf16SpecAlias) ? 0 : (size_t)a.MC)
+                        : (size_t)nseg * a.fpitch;
   const size_t trig = (size_t)Sw * (6 * ((L + 1 + 3) & ~3) + 4);  // TrigLds<L>::kRow per sample
   const size_t lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) + sizeof(float) * (fl + trig);
   if (lds > kTileMaxLds || groups > 0x7fffffff) return false;
@@ -351,6 +363,12 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   p.a.ang_out = ang_out;
   p.a.transpose = transpose ? 1 : 0;
   p.stream = stream;
+  if (p.a.tflags && (reinterpret_cast<uintptr_t>(out) & 3)) {
+    // the bf16-tile options write / read 4-byte words at tile offsets that are 4-byte
+    // aligned only when the output is (2-byte aligned views take the plain tile)
+    if (p.a.tflags & kTileBf16SpecAlias) p.lds += sizeof(float) * (size_t)p.a.MC;
+    p.a.tflags = 0;
+  }
   return dispatch_L<FwdLauncher>(L, p);
 }
 

@@ -28,8 +28,20 @@ struct ActionArgs {
   int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores, 2 = plain (A/B)
   int prio;             // tile kernel wave priority: 2 = prologue at s_setprio 3, chain at 0
                         // (default); A/B: 0 off, 1 flush at 3, 3 = 2 + flush at 2
+  int tflags;           // tile kernel, bf16 tile with compile-time C (kTileBf16* bits)
   int seg_lo[kMaxSeg + 1];
 };
+
+// bf16-tile options of the forward tile kernel (ActionArgs::tflags; compile-time C only):
+//   kTileBf16PairRows   rows i / i+1 leave each lane pair (c even, c+1) as one 4-byte LDS
+//                       write per lane (DPP swap + v_cvt_pk_bf16_f32) instead of two
+//                       2-byte writes that share a dword
+//   kTileBf16SpecAlias  the fp32 spectrum lives in the tile's last two sample slots: degree
+//                       l's (2l+1)·C values split in two halves over the two slots' rows of
+//                       degree l (degree-local: only the wave of degree l touches them, and
+//                       it reads them before it writes its own rows there); no separate
+//                       M·C·4-byte spectrum area
+constexpr int kTileBf16PairRows = 1, kTileBf16SpecAlias = 4;
 
 // ---- fused-prologue maths (per lane, registers).
 
