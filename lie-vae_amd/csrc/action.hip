@@ -209,7 +209,7 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   const bool bt = out_bytes == 2 && a.C == kTileFastC;
   int Sw = 64 / a.C;
   a.tflags = bt ? kEnvBf16 : 0;
-  if (bt && kEnvSw >= 2 && kEnvSw < Sw) Sw = kEnvSw;
+  if (a.C == kTileFastC && kEnvSw >= 2 && kEnvSw < Sw) Sw = kEnvSw;
   if (Sw < 2) a.tflags &= ~kTileBf16SpecAlias;
   const int64_t groups = (a.n + Sw - 1) / Sw;
   double total = 0.0;

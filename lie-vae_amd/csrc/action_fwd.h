@@ -273,7 +273,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   constexpr bool BT = CT > 0 && !FT;  // bf16 tile, compile-time C: a.tflags options
   const bool alias = BT && (a.tflags & kTileBf16SpecAlias);
   const int C = CT > 0 ? CT : a.C;
-  const int Sw = BT ? a.Sw : (CT > 0 ? 64 / CT : a.Sw);
+  const int Sw = a.Sw;  // 64 / C, or fewer (plan: LDS per block vs blocks per CU)
   const int64_t MC = CT > 0 ? (int64_t)(LT + 1) * (LT + 1) * CT : a.MC;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
