@@ -101,6 +101,49 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce2_kernel(const float* w
   if (k == 0 && e < MC) gF[e] = part[0][col];
 }
 
+// Chunk-major slabs (ActionBwdArgs::slab_chunked): one block per 16-element chunk, whose
+// gx slabs are one contiguous run of gx * 64 bytes.  Thread t takes quarter q = t % 4 of
+// every slab b = t / 4, t / 4 + 256, ... (16-byte loads, all issued together), then the 256
+// partials of each quarter are added by a fixed-order halving tree.  Deterministic.
+__global__ __launch_bounds__(1024) void action_bwd_reduce3_kernel(const float* ws_F, float* gF, int64_t MC,
+                                                                  int nslab) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ f4 part[256][4];
+  const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
+  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)blockIdx.x * nslab * kSlabChunk) + q;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  int b = bs;
+  for (; b + 3 * 256 < nslab; b += 4 * 256) {
+    f4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = base[(int64_t)(b + u * 256) * 4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u];
+  }
+  {
+    f4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) v[u] = b + u * 256 < nslab ? base[(int64_t)(b + u * 256) * 4] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (b + u * 256 < nslab) acc += v[u];
+  }
+  part[bs][q] = acc;
+#pragma unroll
+  for (int h = 128; h >= 1; h >>= 1) {
+    __syncthreads();
+    if (bs < h) part[bs][q] += part[bs + h][q];
+  }
+  if (bs == 0) {
+    const f4 r = part[0][q];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = (int64_t)blockIdx.x * kSlabChunk + 4 * q + k;
+      if (e < MC) gF[e] = r[k];
+    }
+  }
+}
+
 namespace {
 
 template <int... Ls>
@@ -396,6 +439,7 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 // profiles/r02_bwd_regbudget_sweep.txt).
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 constexpr int64_t kBwdCUs = 256;  // MI355X compute units
+constexpr int kBwdReduceDefault = 16;  // LV_BWD_REDUCE default (see action_bwd_common)
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
@@ -450,7 +494,8 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       b.gx = (int)std::min<int64_t>(groups, fallback ? kBwdMaxBlocksFallback : kBwdMaxBlocks);
       if (kEnvGlobal && sharedF) b.gx = (int)std::min<int64_t>(groups, kBwdMaxBlocks);
       b.lds = lds;
-      b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)MC : 0;
+      b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)(fmode == kBwdFShared ? slab_chunks(MC) * kSlabChunk : MC)
+                     : 0;
       return true;
     }
   }
@@ -520,6 +565,10 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.a.fpitch = b.fpitch;
   static const int kEnvBwdPrio = LV_KNOB("LV_BWD_PRIO", 0);  // A/B: 2 = prologue-priority phases
   p.a.prio = kEnvBwdPrio;
+  // dF slab reduce: LV_BWD_REDUCE (A/B) 3 = chunk-major slabs + action_bwd_reduce3_kernel,
+  // 16 / 8 / 4 = row slabs + action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
+  static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
+  p.a.slab_chunked = b.fmode == kBwdFShared && kEnvReduce == 3;
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
   p.gx = b.gx;
   p.nseg = b.nseg;
@@ -528,10 +577,13 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.stream = st;
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
-  // dF slab reduce: action_bwd_reduce2_kernel<16> by default (profiles/r03_bwd_reduce_ab.txt:
-  // 17.51 vs 17.89 us per lv_group_action_bwd call at batch 4,096, 9.63 vs 9.75 at 512,
-  // 191.0 vs 191.1 at 65,536); A/B: LV_BWD_REDUCE = 1 the round-2 kernel, 4 / 8 columns
-  static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", 16);
+  // dF slab reduce (profiles/r03_bwd_reduce_ab.txt: reduce2<16> 17.51 vs 17.89 us per
+  // lv_group_action_bwd call at batch 4,096 against the round-2 kernel)
+  if (p.a.slab_chunked) {
+    hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
+                       (const float*)workspace, gF, MC, b.gx);
+    LV_RETURN_LAUNCH("action_bwd_reduce3_kernel");
+  }
   if (kEnvReduce == 8) {
     hipLaunchKernelGGL(action_bwd_reduce2_kernel<8>, dim3(ceil_div(MC, 8)), dim3(1024), 0, st,
                        (const float*)workspace, gF, MC, b.gx);

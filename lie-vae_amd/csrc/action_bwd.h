@@ -49,8 +49,15 @@ struct ActionBwdArgs {
   int C, Sw, transpose;
   int fpitch;          // floats per wave-private spectrum slice in LDS
   int prio;            // 2: group load + prologue at s_setprio 3, chain at 0 (A/B: 0 off)
+  int slab_chunked;    // kBwdFShared slab layout: 0 [block][M*C], 1 [M*C/16][block][16]
   int seg_lo[kMaxSeg + 1];
 };
+
+// Chunk-major dF slabs (slab_chunked): element e of block b at
+// ((e / 16) * gridDim.x + b) * 16 + e % 16, so that the reduce reads each 16-element chunk's
+// slabs as one contiguous run (action_bwd_reduce3_kernel).
+constexpr int kSlabChunk = 16;
+__host__ __device__ inline int64_t slab_chunks(int64_t MC) { return (MC + kSlabChunk - 1) / kSlabChunk; }
 
 // LDS floats of the backward tile kernel beyond the gout tile.
 __host__ __device__ inline int bwd_trig_floats(int Sw, int L) {
@@ -368,8 +375,17 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     block_sync_lds();  // the next group overwrites the tile, the table and the partials
   }
   if constexpr (FM == kBwdFShared) {
-    float* slab = a.ws_F + (int64_t)blockIdx.x * MC;
-    for (int e = lane; e < fcnt; e += 64) slab[rows_lo * C + e] = slabL[rows_lo * C + e];
+    if (a.slab_chunked) {
+      float* ws = a.ws_F + (int64_t)blockIdx.x * kSlabChunk;
+      const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
+      for (int e = lane; e < fcnt; e += 64) {
+        const int g = rows_lo * C + e;
+        ws[(g / kSlabChunk) * cstride + g % kSlabChunk] = slabL[g];
+      }
+    } else {
+      float* slab = a.ws_F + (int64_t)blockIdx.x * MC;
+      for (int e = lane; e < fcnt; e += 64) slab[rows_lo * C + e] = slabL[rows_lo * C + e];
+    }
   }
 }
 
