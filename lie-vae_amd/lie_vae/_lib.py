@@ -158,6 +158,11 @@ def stream():
     return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device())
 
 
+def stream_of(device):
+    """The current HIP stream of a tensor's device (raw handle, as an int)."""
+    return torch._C._cuda_getCurrentRawStream(device.index)
+
+
 def ptr(t):
     return t.data_ptr() if t is not None else None
 

@@ -214,7 +214,7 @@ def _bwd_workspace(n, L, C, shared, device):
     nb = _WS_BYTES.get(key)
     if nb is None:
         nb = _WS_BYTES[key] = int(_lib.load().lv_group_action_bwd_workspace(n, L, C, shared))
-    st = stream()
+    st = _lib.stream_of(device)
     if torch.cuda.is_current_stream_capturing():
         return torch.empty(max(nb, 1), device=device, dtype=torch.uint8), nb, st
     bkey = (device.index, st)
@@ -286,38 +286,47 @@ def _contig(t):
     return t.contiguous() if t.dtype == F32 else t.float().contiguous()
 
 
+def _f32c(t):
+    """t itself when already fp32 and contiguous (the common case: no dispatcher call)."""
+    return t if t.dtype == F32 and t.is_contiguous() else t.to(F32).contiguous()
+
+
 class _FusedExpAction(torch.autograd.Function):
     """mu@exp(v) -> ZYZ -> block D·F in one launch; backward = one tile-kernel launch
-    (group-action backward with the exp -> ZYZ VJP in its tail) + the dF slab reduce."""
+    (group-action backward with the exp -> ZYZ VJP in its tail) + the dF slab reduce.
+    Host path kept short (the eager training direction is host-bound at config 2): no
+    conversion calls on already-fp32 contiguous inputs, the workspace cached per stream."""
 
     @staticmethod
     def forward(ctx, mu, v, spec, L, transpose, out_dtype):
-        v = _prep(v)
+        v = _f32c(v)
         n = v.shape[0]
-        mu_c = _prep(mu) if mu is not None else None
+        mu_c = _f32c(mu) if mu is not None else None
         M = (L + 1) ** 2
         C = spec.shape[-1]
-        stride = 0 if spec.dim() == 2 else M * C
-        dt = _lib.LV_DTYPE_BF16 if out_dtype == torch.bfloat16 else _lib.LV_DTYPE_F32
-        out = _empty((n, M, C), v, out_dtype)
-        ang = _empty((n, 3), v)
-        call("lv_fused_exp_action_fwd", ptr(mu_c), ptr(v), ptr(spec), stride, ptr(out), dt,
-             ptr(ang), n, L, C, int(transpose), stream())
+        dev = v.device
+        out = torch.empty((n, M, C), device=dev, dtype=out_dtype)
+        ang = torch.empty((n, 3), device=dev, dtype=F32)
+        call("lv_fused_exp_action_fwd", None if mu_c is None else mu_c.data_ptr(), v.data_ptr(),
+             spec.data_ptr(), 0, out.data_ptr(),
+             _lib.LV_DTYPE_BF16 if out_dtype == torch.bfloat16 else _lib.LV_DTYPE_F32,
+             ang.data_ptr(), n, L, C, int(transpose), _lib.stream_of(dev))
         ctx.save_for_backward(mu_c, v, spec, ang)
-        ctx.has_mu, ctx.L, ctx.transpose, ctx.stride = mu is not None, L, transpose, stride
+        ctx.L, ctx.transpose = L, transpose
         return out
 
     @staticmethod
     def backward(ctx, gout):
         mu, v, spec, ang = ctx.saved_tensors
         n, L, C = v.shape[0], ctx.L, spec.shape[-1]
-        gout = _prep(gout)
-        gspec = torch.empty_like(spec)
-        ws, ws_bytes, st = _bwd_workspace(n, L, C, 1, v.device)
-        gv = torch.empty_like(v)
-        gmu = torch.empty_like(mu) if ctx.has_mu else None
-        call("lv_fused_exp_action_bwd", ptr(mu), v.data_ptr(), ang.data_ptr(), spec.data_ptr(),
-             gout.data_ptr(), ptr(gmu), gv.data_ptr(), gspec.data_ptr(), n, L, C,
+        gout = _f32c(gout)
+        dev = v.device
+        gspec, gv = torch.empty_like(spec), torch.empty_like(v)
+        gmu = torch.empty_like(mu) if mu is not None else None
+        ws, ws_bytes, st = _bwd_workspace(n, L, C, 1, dev)
+        call("lv_fused_exp_action_bwd", None if mu is None else mu.data_ptr(), v.data_ptr(),
+             ang.data_ptr(), spec.data_ptr(), gout.data_ptr(),
+             None if gmu is None else gmu.data_ptr(), gv.data_ptr(), gspec.data_ptr(), n, L, C,
              int(ctx.transpose), ws.data_ptr(), ws_bytes, st)
         return gmu, gv, gspec, None, None, None
 
@@ -335,7 +344,7 @@ def fused_exp_action(mu, v, spectrum, L, transpose=False, out_dtype=F32):
         raise ValueError("fused_exp_action takes a shared (M,C) spectrum; use group_action "
                          "for a per-sample (n,M,C) spectrum")
     _lib.require_device(v, spectrum, mu)
-    return _FusedExpAction.apply(mu, v, _contig(spectrum), L, transpose, out_dtype)
+    return _FusedExpAction.apply(mu, v, _f32c(spectrum), L, transpose, out_dtype)
 
 
 def wigner_blocks(angles, L):
