@@ -440,6 +440,7 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 constexpr int64_t kBwdCUs = 256;  // MI355X compute units
 constexpr int kBwdReduceDefault = 16;  // LV_BWD_REDUCE default (see action_bwd_common)
+constexpr int kBwdVariantDefault = 0;  // LV_BWD_VARIANT default (kBwdVar* bits)
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
@@ -569,6 +570,8 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // 16 / 8 / 4 = row slabs + action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
   static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
   p.a.slab_chunked = b.fmode == kBwdFShared && kEnvReduce == 3;
+  static const int kEnvVariant = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
+  p.a.variant = kEnvVariant;
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
   p.gx = b.gx;
   p.nseg = b.nseg;

@@ -31,6 +31,7 @@ namespace lv {
 // for tiles too large to leave room for both (large C at high l); same summation order,
 // so bitwise equal to kBwdFShared for the same plan.
 constexpr int kBwdFSample = 0, kBwdFShared = 1, kBwdFSharedGlobal = 2;
+constexpr int kBwdVarJit = 1;  // ActionBwdArgs::variant: row-pair reads of F and G (wide kernel)
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
@@ -50,6 +51,7 @@ struct ActionBwdArgs {
   int fpitch;          // floats per wave-private spectrum slice in LDS
   int prio;            // 2: group load + prologue at s_setprio 3, chain at 0 (A/B: 0 off)
   int slab_chunked;    // kBwdFShared slab layout: 0 [block][M*C], 1 [M*C/16][block][16]
+  int variant;         // kernel variant bits (kBwdVar*)
   int seg_lo[kMaxSeg + 1];
 };
 
@@ -111,6 +113,38 @@ __device__ __forceinline__ void xm_t(const Mult<l>& m, const float (&x)[2 * l + 
     else y[i] = fmaf(m.c[-f], x[i], m.s[-f] * x[2 * l - i]);
   });
 }
+// y = X x / y = X^T x with x read from memory (LDS) in row pairs (i, 2l-i) right where the
+// product needs them: no (2l+1)-register copy of x stays live beside the chain's arrays.
+// Same arithmetic as xm / xm_t.
+template <int l, bool T>
+__device__ __forceinline__ void xm_mem(const Mult<l>& m, const float* x, int stride, float (&y)[2 * l + 1]) {
+  sfor<l>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    const float a = x[i * stride], b = x[(2 * l - i) * stride];
+    if constexpr (T) {
+      y[i] = fmaf(m.c[f], a, -(m.s[f] * b));
+      y[2 * l - i] = fmaf(m.c[f], b, m.s[f] * a);
+    } else {
+      y[i] = fmaf(m.c[f], a, m.s[f] * b);
+      y[2 * l - i] = fmaf(m.c[f], b, -(m.s[f] * a));
+    }
+  });
+  y[l] = x[l * stride];
+}
+// <a, K x> with x read from memory in row pairs (kdot's arithmetic)
+template <int l>
+__device__ __forceinline__ float kdot_mem(const float (&av)[2 * l + 1], const float* x, int stride) {
+  float acc = 0.f;
+  sfor<l>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    const float t = fmaf(av[i], x[(2 * l - i) * stride], -(av[2 * l - i] * x[i * stride]));
+    acc = fmaf((float)f, t, acc);
+  });
+  return acc;
+}
+
 // <a, K b> with K = X(θ)^{-1} dX/dθ, the so(2) generator of the degree-l block: row i
 // of K has f_i = l - i at column 2l-i (X = C + S P with P the row reversal, so
 // dX/dθ = diag(f cos) P - diag(f sin) = X diag(f) P).  Hence <g, X' x> = <X^T g, K x>:
@@ -145,7 +179,9 @@ __host__ __device__ constexpr bool bwd_wide(int L, int C, int fmode, int64_t gro
 // profiles/r02_bwd_regbudget_sweep.txt), so the launcher uses it whenever the grid covers
 // the batch.
 // WPE: waves per SIMD the register budget is sized for (3 only for the bwd_wide case).
-template <int LT, int CT, int FM, bool LOOP = true, int WPE = 2>
+// JIT: the spectrum column and G read in row pairs inside the products (A/B variant bit
+// kBwdVarJit of ActionBwdArgs::variant; wide kernel only).
+template <int LT, int CT, int FM, bool LOOP = true, int WPE = 2, bool JIT = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void action_bwd_tile_kernel(ActionBwdArgs a) {
   constexpr bool SHAREDF = FM != kBwdFSample;
@@ -273,33 +309,41 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         constexpr int r0 = l * l;
         // live arrays kept to three or four of 2l+1: the spectrum column and G are
         // re-read from LDS where they are needed again
-        float p2[nn], p4[nn], gq[nn], u[nn];
-        {
+        float p2[nn], p4[nn], u[nn];
+        const float* fcol = SHAREDF ? Fl + r0 * fstep : Fs + r0 * C;
+        const int fst = SHAREDF ? fstep : C;
+        if constexpr (JIT) {
+          // the spectrum column and G read in row pairs inside the products that use them
+          // (xm_mem), on every lane: an idle lane's addresses stay inside the block's LDS
+          // and its results are never used
+          xm_mem<l, false>(mult_lds<l, 2, LT>(tj), fcol, fst, u);  // P1
+        } else {
           float f0[nn];
-          sfor<nn>([&](auto K) {
-            constexpr int k = LV_CV(K);
-            f0[k] = SHAREDF ? Fl[(r0 + k) * fstep] : Fs[(r0 + k) * C];
-          });
+          sfor<nn>([&](auto K) { f0[LV_CV(K)] = fcol[LV_CV(K) * fst]; });
           xm<l>(mult_lds<l, 2, LT>(tj), f0, u);   // P1
         }
         jmul<l>(u, p2);                           // P2
         xm<l>(mult_lds<l, 1, LT>(tj), p2, u);     // P3
         jmul<l>(u, p4);                           // P4
-        sfor<nn>([&](auto K) { gq[LV_CV(K)] = active ? tile_lane[(r0 + LV_CV(K)) * C] : 0.f; });
-        xm_t<l>(mult_lds<l, 0, LT>(tj), gq, u);  // Q4
+        if constexpr (JIT) {
+          xm_mem<l, true>(mult_lds<l, 0, LT>(tj), tile_lane + r0 * C, C, u);  // Q4
+        } else {
+          float gq[nn];
+          sfor<nn>([&](auto K) { gq[LV_CV(K)] = active ? tile_lane[(r0 + LV_CV(K)) * C] : 0.f; });
+          xm_t<l>(mult_lds<l, 0, LT>(tj), gq, u);  // Q4
+        }
         ga += kdot<l>(u, p4);                     // <G, Xa' P4> = <Q4, K P4>
         jmul<l>(u, p4);                           // Q3 (reuse p4)
         xm_t<l>(mult_lds<l, 1, LT>(tj), p4, u);  // Q2
         gb += kdot<l>(u, p2);                     // <Q3, Xb' P2> = <Q2, K P2>
         jmul<l>(u, p2);                           // Q1 (reuse p2)
         xm_t<l>(mult_lds<l, 2, LT>(tj), p2, u);  // dF column
-        {
+        if constexpr (JIT) {
+          gc += kdot_mem<l>(u, fcol, fst);        // <Q1, Xc' F> = <dF, K F>
+        } else {
           float f0[nn];
-          sfor<nn>([&](auto K) {
-            constexpr int k = LV_CV(K);
-            f0[k] = SHAREDF ? Fl[(r0 + k) * fstep] : Fs[(r0 + k) * C];
-          });
-          gc += kdot<l>(u, f0);                   // <Q1, Xc' F> = <dF, K F>
+          sfor<nn>([&](auto K) { f0[LV_CV(K)] = fcol[LV_CV(K) * fst]; });
+          gc += kdot<l>(u, f0);
         }
         if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
         if constexpr (SHAREDF) {
@@ -411,8 +455,12 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
   else if (p.fmode == kBwdFSharedGlobal)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSharedGlobal>), grid, block, p.lds, p.stream, p.a);
   else if (bwd_wide(LT, p.a.C, p.fmode, p.a.groups, p.gx)) {
-    if constexpr (LT <= kBwdWideMaxL)
-      hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false, 3>), grid, block, p.lds, p.stream, p.a);
+    if constexpr (LT <= kBwdWideMaxL) {
+      if (p.a.variant & kBwdVarJit)
+        hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false, 3, true>), grid, block, p.lds, p.stream, p.a);
+      else
+        hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false, 3>), grid, block, p.lds, p.stream, p.a);
+    }
   } else if (p.a.C == kTileFastC && p.gx >= p.a.groups)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, kTileFastC, kBwdFShared, false>), grid, block, p.lds, p.stream, p.a);
   else if (p.a.C == kTileFastC)
