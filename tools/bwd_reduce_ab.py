@@ -50,9 +50,11 @@ def main():
         ref = None
         knobs = os.environ.get("AB_KNOBS", "LV_BWD_REDUCE=1,LV_BWD_REDUCE=16,LV_BWD_REDUCE=8,LV_BWD_REDUCE=4,LV_BWD_REDUCE=1")
         for kv in knobs.split(","):
-            name, knob = kv.split("=")
-            path = f"gpurun_out/gF_{B}_{name}_{knob}.npy"
-            env = dict(os.environ, **{name: knob},
+            # one variant: NAME=val, or several joined by '+' (NAME=val+NAME2=val2)
+            pairs = dict(x.split("=") for x in kv.split("+"))
+            name, knob = "+".join(pairs), "+".join(pairs.values())
+            path = f"gpurun_out/gF_{B}_{kv.replace('+', '_')}.npy"
+            env = dict(os.environ, **pairs,
                        LIEVAE_HIP_LIB=os.path.abspath("lie-vae_amd/lie_vae/liblievae_hip_ab.so"))
             r = subprocess.run([sys.executable, "-c", CHILD, str(B), path], env=env,
                                capture_output=True, text=True, timeout=120)
