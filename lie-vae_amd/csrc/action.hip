@@ -486,7 +486,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       const size_t lds = (size_t)tile_stage_bytes(Sw, MC, 4) +
                          sizeof(float) * ((size_t)bwd_trig_floats(Sw, L) + (size_t)nseg * 64 * 3 +
                                           (fmode == kBwdFShared ? (size_t)MC : 0) +
-                                          (size_t)nseg * b.fpitch);
+                                          (size_t)nseg * b.fpitch + 12 * (size_t)Sw);
       if (lds > cap) continue;
       b.Sw = Sw;
       b.nseg = nseg;

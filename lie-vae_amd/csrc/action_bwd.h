@@ -172,6 +172,23 @@ __host__ __device__ constexpr bool bwd_wide(int L, int C, int fmode, int64_t gro
   return L <= kBwdWideMaxL && C == kTileFastC && fmode == kBwdFShared && gx >= groups;
 }
 
+// This block's dF slab elements [g0, g0 + cnt) (a wave's rows) from LDS to the workspace,
+// row layout ([block][M*C]) or chunk-major (slab_chunked).
+__device__ __forceinline__ void write_slab_rows(const ActionBwdArgs& a, const float* slabL, int g0, int cnt,
+                                                int lane) {
+  if (a.slab_chunked) {
+    float* ws = a.ws_F + (int64_t)blockIdx.x * kSlabChunk;
+    const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
+    for (int e = lane; e < cnt; e += 64) {
+      const int g = g0 + e;
+      ws[(g / kSlabChunk) * cstride + g % kSlabChunk] = slabL[g];
+    }
+  } else {
+    float* slab = a.ws_F + (int64_t)blockIdx.x * a.MC;
+    for (int e = lane; e < cnt; e += 64) slab[g0 + e] = slabL[g0 + e];
+  }
+}
+
 // LOOP: blocks loop over sample groups (grid capped, bounded workspace).  Without it each
 // block takes exactly one group (grid = groups): the group loop made the compiler hoist
 // loop-invariant addresses and hold them across the whole chain (256 VGPRs + 240 B/lane of
@@ -202,6 +219,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   const int frows = fseg_rows(lo, hi);
   const int stage_bytes = tile_stage_bytes(Sw, MC, 4);
   // LDS: [gout / dF tile][multiples table][angle partials][dF slab (shared F)][F slices]
+  //      [fused path: the group's v (and mu), Sw * 12 floats]
   float* trig = lds + (stage_bytes >> 2);
   float* apart = trig + bwd_trig_floats(Sw, LT);               // [nseg][64][3]
   // dF slab: LDS [M*C] (kBwdFShared), or this block's workspace row (kBwdFSharedGlobal)
@@ -243,6 +261,9 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       }
     }
   }
+  // fused path: the exp -> ZYZ VJP's inputs, loaded by the prologue threads so that the
+  // tail does not wait on global loads (after the last spectrum slice)
+  float* vmu = apart + (nthr >> 6) * 64 * 3 + (FM == kBwdFShared ? (int)MC : 0) + (nthr >> 6) * a.fpitch;
   const float* Fl = GSLAB ? a.F + c : (CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo);
   const int fstep = (GSLAB || CT > 0) ? C : 1;
   const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
@@ -292,6 +313,11 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         for (int i = 0; i < 3; ++i) { c1[i] = cc[i]; s1[i] = ss[i]; }
       }
       trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
+    }
+    if (a.v && tid < 12 * Sv) {  // v (3) and mu (9) of the group's samples for the VJP tail
+      const int js = tid / 12, k = tid - 12 * js;
+      if (k < 3) vmu[js * 12 + k] = a.v[(s0 + js) * 3 + k];
+      else if (a.mu) vmu[js * 12 + k] = a.mu[(s0 + js) * 9 + (k - 3)];
     }
     // 3. the LDS-DMA writes of this wave have landed (an LDS-DMA is counted in vmcnt)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -374,6 +400,11 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         }
       }
     });
+    if constexpr (FM == kBwdFShared && !LOOP) {
+      // one group per block: this wave's slab rows are final -- write them now, ahead of
+      // the angle-gradient tail
+      write_slab_rows(a, slabL, rows_lo * C, fcnt, lane);
+    }
     // angle gradients: sum over the C lanes of a sample (column order), then segments
     float* ap = apart + wave * 64 * 3;
     if (a.transpose) {
@@ -394,16 +425,18 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       if (a.gang) a.gang[(s0 + js) * 3 + i] = r;
       if (a.v) trig[js * 3 + i] = r;  // the chains are done: the table is free
     }
+    if (!LOOP && SHAREDF && wave > 0) return;  // the tail below is wave 0's (tid < 3 * Sw)
     if (a.v) {  // fused path: exp -> ZYZ VJP of the group's samples (exp_eazyz_vjp_sample)
-      block_sync_lds();
+      if constexpr (!LOOP && SHAREDF) wave_lds_sync();  // wave 0 alone from here
+      else block_sync_lds();
       if (tid < Sv) {
         const int64_t s = s0 + tid;
         float av[3], g[3], m[9], gm[9], o[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { av[k] = a.v[s * 3 + k]; g[k] = trig[tid * 3 + k]; }
+        for (int k = 0; k < 3; ++k) { av[k] = vmu[tid * 12 + k]; g[k] = trig[tid * 3 + k]; }
         if (a.mu) {
 #pragma unroll
-          for (int k = 0; k < 9; ++k) m[k] = a.mu[s * 9 + k];
+          for (int k = 0; k < 9; ++k) m[k] = vmu[tid * 12 + 3 + k];
         }
         exp_eazyz_vjp_sample(av, a.mu ? m : nullptr, g, gm, o);
         if (a.mu) {
@@ -416,21 +449,10 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     }
     if constexpr (!SHAREDF)
       tile_flush<float, 1>(a.gF + s0 * MC, stage_b, mis, nbytes, tid, nthr);
+    if constexpr (!LOOP && SHAREDF) return;
     block_sync_lds();  // the next group overwrites the tile, the table and the partials
   }
-  if constexpr (FM == kBwdFShared) {
-    if (a.slab_chunked) {
-      float* ws = a.ws_F + (int64_t)blockIdx.x * kSlabChunk;
-      const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
-      for (int e = lane; e < fcnt; e += 64) {
-        const int g = rows_lo * C + e;
-        ws[(g / kSlabChunk) * cstride + g % kSlabChunk] = slabL[g];
-      }
-    } else {
-      float* slab = a.ws_F + (int64_t)blockIdx.x * MC;
-      for (int e = lane; e < fcnt; e += 64) slab[rows_lo * C + e] = slabL[rows_lo * C + e];
-    }
-  }
+  if constexpr (FM == kBwdFShared) write_slab_rows(a, slabL, rows_lo * C, fcnt, lane);
 }
 
 // Slab count per block of action_bwd_reduce_kernel (defined in action.hip).
