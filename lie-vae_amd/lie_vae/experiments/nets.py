@@ -15,6 +15,8 @@ MFMA; bf16 under autocast) instead of MIOpen's convolution solvers; any other in
 shape takes the convolution.  ``GEMM_LAYERS = False`` before building a model restores
 plain convolutions (A/B).
 """
+import contextlib
+
 import torch
 from torch import nn
 from torch.nn import functional as F
@@ -24,6 +26,56 @@ GEMM_LAYERS = True
 
 def _cl(t):
     return t.dim() == 4 and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
+
+
+# ---- bf16 copies of the conv parameters, refreshed once per optimizer step
+# Under bf16 autocast every conv / deconv casts its fp32 weight and bias to bf16 on every
+# forward (one copy kernel per tensor: 24 per config-3 step).  Bf16ParamCache keeps bf16
+# copies that DPTrainer refreshes with ONE multi-tensor copy after each optimizer step; a
+# layer uses its copy only while it is current (same storage, same in-place version as at
+# the refresh), else it casts as before.  The copy enters autograd through _CachedCast,
+# whose backward is the cast's (gradient to fp32).
+class _CachedCast(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p, pb):
+        ctx.dt = p.dtype
+        return pb.view_as(pb)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dt), None
+
+
+def bf16_param(p):
+    """p as bf16: the cached copy while it is current, else p.to(bfloat16)."""
+    if p is None:
+        return None
+    e = getattr(p, "_lv_bf16", None)
+    if e is not None and e[1] == p._version and e[2] == p.data_ptr():
+        return _CachedCast.apply(p, e[0])
+    return p.to(torch.bfloat16)
+
+
+class Bf16ParamCache:
+    """bf16 copies of the weights and biases of a model's convolution layers (the tensors
+    autocast would cast per forward); refresh() after every optimizer step."""
+
+    def __init__(self, model):
+        self.src = [p for m in model.modules() if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d))
+                    for p in (m.weight, m.bias) if p is not None and p.dtype == torch.float32]
+        self.dst = [torch.empty_like(p, dtype=torch.bfloat16) for p in self.src]
+        self.refresh()
+
+    @torch.no_grad()
+    def refresh(self):
+        if self.src:
+            torch._foreach_copy_(self.dst, self.src)
+        for p, d in zip(self.src, self.dst):
+            p._lv_bf16 = (d, p._version, p.data_ptr())
+
+
+def _autocast_bf16():
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
 
 class GemmConvTranspose2d(nn.ConvTranspose2d):
@@ -39,14 +91,19 @@ class GemmConvTranspose2d(nn.ConvTranspose2d):
             return super().forward(x, output_size)
         B, (k0, k1) = x.shape[0], self.kernel_size
         cl = _cl(self.weight)
+        ac = _autocast_bf16()  # bf16 autocast: the cached bf16 parameters, explicit bf16 GEMM
+        weight, bias = (bf16_param(self.weight), bf16_param(self.bias)) if ac else (self.weight, self.bias)
         # W (c_in, c_out, k0, k1) -> columns (o, i, j) [NCHW out] or (i, j, o) [NHWC out]
-        w = (self.weight.permute(0, 2, 3, 1) if cl else self.weight).reshape(self.in_channels, -1)
+        w = (weight.permute(0, 2, 3, 1) if cl else weight).reshape(self.in_channels, -1)
         xm = x.reshape(B, self.in_channels)
-        if self.bias is None:
-            y = xm @ w
-        else:
-            b = self.bias.repeat(k0 * k1) if cl else self.bias.repeat_interleave(k0 * k1)
-            y = torch.addmm(b, xm, w)
+        with torch.autocast("cuda", enabled=False) if ac else contextlib.nullcontext():
+            if ac:
+                xm = xm.to(torch.bfloat16)
+            if bias is None:
+                y = xm @ w
+            else:
+                b = bias.repeat(k0 * k1) if cl else bias.repeat_interleave(k0 * k1)
+                y = torch.addmm(b, xm, w)
         if cl:
             return y.view(B, k0, k1, self.out_channels).permute(0, 3, 1, 2)
         return y.view(B, self.out_channels, k0, k1)
@@ -66,13 +123,16 @@ class GemmConv2d(nn.Conv2d):
         if not self._gemm_shape(x):
             return super().forward(x)
         B = x.shape[0]
+        ac = _autocast_bf16()
+        weight, bias = (bf16_param(self.weight), bf16_param(self.bias)) if ac else (self.weight, self.bias)
         if _cl(x):  # NHWC memory: flatten (i, j, c) without a copy, reorder the weight
             xm = x.permute(0, 2, 3, 1).reshape(B, -1)
-            w = self.weight.permute(0, 2, 3, 1).reshape(self.out_channels, -1)
+            w = weight.permute(0, 2, 3, 1).reshape(self.out_channels, -1)
         else:
             xm = x.reshape(B, -1)
-            w = self.weight.reshape(self.out_channels, -1)
-        y = torch.nn.functional.linear(xm, w, self.bias)
+            w = weight.reshape(self.out_channels, -1)
+        with torch.autocast("cuda", enabled=False) if ac else contextlib.nullcontext():
+            y = torch.nn.functional.linear(xm.to(torch.bfloat16) if ac else xm, w, bias)
         return y.view(B, self.out_channels, 1, 1)
 
 
@@ -354,7 +414,7 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
             xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             if self.input_is_relu and not small:
                 xb = F_.relu(xb)
-            y = _Deconv4s2.apply(xb, self.weight.to(torch.bfloat16),
+            y = _Deconv4s2.apply(xb, bf16_param(self.weight),
                                  None if self.bias is None else self.bias.float(), flags)
             return F_.relu(y) if self.relu_out and small else y
 
@@ -419,14 +479,18 @@ class MfmaDgradConv2d(nn.Conv2d):
                 and self.in_channels <= 208 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
 
     def forward(self, x):
-        bf16 = x.dtype == torch.bfloat16 or (
-            torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        ac = _autocast_bf16()
+        bf16 = x.dtype == torch.bfloat16 or ac
         if not bf16 or not self._ok(x):
-            return super().forward(x)
+            if not ac or self.padding_mode != "zeros":
+                return super().forward(x)
+            with torch.autocast("cuda", enabled=False):  # autocast's conv, cached bf16 params
+                return torch.nn.functional.conv2d(x.to(torch.bfloat16), bf16_param(self.weight),
+                                                  bf16_param(self.bias), self.stride, self.padding,
+                                                  self.dilation, self.groups)
         with torch.autocast("cuda", enabled=False):
             xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            return _Conv4s2.apply(xb, self.weight.to(torch.bfloat16),
-                                  None if self.bias is None else self.bias.to(torch.bfloat16))
+            return _Conv4s2.apply(xb, bf16_param(self.weight), bf16_param(self.bias))
 
 
 def _conv(*a):

@@ -182,6 +182,12 @@ class DPTrainer:
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay,
                                     capturable=graph, fused=True if fused_adam else None)
         self._graph = None
+        # bf16 autocast: the conv parameters' bf16 copies, refreshed by one multi-tensor
+        # copy after each optimizer step instead of one cast kernel per tensor per forward
+        self.bf16_params = None
+        if amp_dtype == torch.bfloat16 and all(p.is_cuda for p in model.parameters()):
+            from .nets import Bf16ParamCache
+            self.bf16_params = Bf16ParamCache(model)
 
     def loss(self, x, eps=None, beta=1.0):
         if self.amp_dtype is not None:
@@ -229,6 +235,8 @@ class DPTrainer:
         if self.clip:
             torch.nn.utils.clip_grad_norm_(self.clip_params(), self.clip)
         self.opt.step()
+        if self.bf16_params is not None:
+            self.bf16_params.refresh()
         return loss.detach(), recon.detach(), kl.detach()
 
     # ------------------------------------------------------------ graph capture
@@ -307,6 +315,8 @@ class DPTrainer:
                     for t in self.opt.state.get(p, {}).values():
                         if torch.is_tensor(t):
                             t.zero_()
+        if self.bf16_params is not None:  # the graph's forward reads the copies: re-derive
+            self.bf16_params.refresh()
         self._graph = graph
 
         def replay(x_new=None, eps_new=None):
