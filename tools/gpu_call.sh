@@ -13,6 +13,8 @@
 #   prof-driver  rocprofv3 --kernel-trace --stats of the driver-form bench
 #   train        bench_train.py config 3, bf16 channels-last, and the fp32 step
 #   rehearse     the N-rank rehearsal (two ranks sharing the GPU, gloo)
+#   ab-c5        config-5 bf16 tile-option variants (AB_C5 overrides the list)
+#   ab-bwd       backward knob variants (AB_KNOBS, AB_BATCHES override)
 # Every GPU step runs under its own time limit; a fault, abort or time-limit kill ends
 # the call there (no retries).
 set -u
@@ -77,6 +79,14 @@ for s in "$@"; do
       grep '^{' "$OUT/train_f32.log" | cut -c1-240 ;;
     rehearse)
       step rehearse 600 bash tools/gpu_rehearse_ranks.sh ;;
+    ab-c5)  # config-5 bf16 tile options (AB_C5 = the variant specs of tools/gpu_variants.sh)
+      step ab_c5 900 bash tools/gpu_variants.sh "--lmax 20 --batch 8192 --dtype bf16 --sweep=65536" \
+        ${AB_C5:-base= pair=LV_TILE_BF16=1 alias=LV_TILE_BF16=4 both=LV_TILE_BF16=5 sw5=LV_TILE_SW=5 alias_sw5=LV_TILE_BF16=4,LV_TILE_SW=5}
+      cat "$OUT/ab_c5.log" ;;
+    ab-bwd)  # backward knob variants (AB_KNOBS, tools/bwd_reduce_ab.py) at AB_BATCHES
+      step ab_bwd 900 env AB_KNOBS="${AB_KNOBS:-LV_BWD_REDUCE=16,LV_BWD_REDUCE=3,LV_BWD_VARIANT=1,LV_BWD_REDUCE=3+LV_BWD_VARIANT=1,LV_BWD_REDUCE=16}" \
+        python tools/bwd_reduce_ab.py ${AB_BATCHES:-4096 512 65536}
+      cat "$OUT/ab_bwd.log" ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
