@@ -439,7 +439,7 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 // profiles/r02_bwd_regbudget_sweep.txt).
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 constexpr int64_t kBwdCUs = 256;  // MI355X compute units
-constexpr int kBwdReduceDefault = 16;  // LV_BWD_REDUCE default (see action_bwd_common)
+constexpr int kBwdReduceDefault = 3;  // LV_BWD_REDUCE default (see action_bwd_common)
 constexpr int kBwdVariantDefault = 0;  // LV_BWD_VARIANT default (kBwdVar* bits)
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
@@ -495,8 +495,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       b.gx = (int)std::min<int64_t>(groups, fallback ? kBwdMaxBlocksFallback : kBwdMaxBlocks);
       if (kEnvGlobal && sharedF) b.gx = (int)std::min<int64_t>(groups, kBwdMaxBlocks);
       b.lds = lds;
-      b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)(fmode == kBwdFShared ? slab_chunks(MC) * kSlabChunk : MC)
-                     : 0;
+      b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk) : 0;
       return true;
     }
   }
@@ -569,7 +568,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // dF slab reduce: LV_BWD_REDUCE (A/B) 3 = chunk-major slabs + action_bwd_reduce3_kernel,
   // 16 / 8 / 4 = row slabs + action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
   static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
-  p.a.slab_chunked = b.fmode == kBwdFShared && kEnvReduce == 3;
+  p.a.slab_chunked = b.fmode != kBwdFSample && kEnvReduce == 3;
   static const int kEnvVariant = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
   p.a.variant = kEnvVariant;
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
@@ -580,8 +579,11 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.stream = st;
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
-  // dF slab reduce (profiles/r03_bwd_reduce_ab.txt: reduce2<16> 17.51 vs 17.89 us per
-  // lv_group_action_bwd call at batch 4,096 against the round-2 kernel)
+  // dF slab reduce: chunk-major slabs + action_bwd_reduce3_kernel by default
+  // (profiles/r04_bwd_reduce_ab.txt: 16.0 vs 18.0 us per lv_group_action_bwd call at batch
+  // 4,096, 187 vs 191 at 65,536, 9.9 vs 9.8 at 512 against reduce2<16>, the round-3
+  // default; an in-kernel reduction by the tile kernel's last blocks -- completion counter,
+  // device-scope release fences -- ran 75 us per call at 4,096 and was dropped)
   if (p.a.slab_chunked) {
     hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
                        (const float*)workspace, gF, MC, b.gx);

@@ -224,13 +224,22 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   float* apart = trig + bwd_trig_floats(Sw, LT);               // [nseg][64][3]
   // dF slab: LDS [M*C] (kBwdFShared), or this block's workspace row (kBwdFSharedGlobal)
   float* slabL = GSLAB ? a.ws_F + (int64_t)blockIdx.x * MC : apart + (nthr >> 6) * 64 * 3;
+  // slab element g: LDS (kBwdFShared), or this block's workspace slab in the row or the
+  // chunk-major layout (kBwdFSharedGlobal; the layout the reduce kernel reads)
+  auto slab_at = [&](int g) -> float& {
+    if constexpr (GSLAB) {
+      if (a.slab_chunked)
+        return a.ws_F[((int64_t)(g / kSlabChunk) * gridDim.x + blockIdx.x) * kSlabChunk + g % kSlabChunk];
+    }
+    return slabL[g];
+  };
   float* Fw = apart + (nthr >> 6) * 64 * 3 + (FM == kBwdFShared ? (int)MC : 0) + wave * a.fpitch;
   // spectrum slice (shared F): once per block
   constexpr int kFPer = 6;
   const int fcnt = SHAREDF ? (hi * hi - rows_lo) * C : 0;
   const float* fsrc = a.F + rows_lo * C;
   if constexpr (GSLAB) {
-    for (int e = lane; e < fcnt; e += 64) slabL[rows_lo * C + e] = 0.f;  // this wave's rows
+    for (int e = lane; e < fcnt; e += 64) slab_at(rows_lo * C + e) = 0.f;  // this wave's rows
   } else if constexpr (SHAREDF) {
     float fv[kFPer];
 #pragma unroll
@@ -314,10 +323,13 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       }
       trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
     }
-    if (a.v && tid < 12 * Sv) {  // v (3) and mu (9) of the group's samples for the VJP tail
-      const int js = tid / 12, k = tid - 12 * js;
-      if (k < 3) vmu[js * 12 + k] = a.v[(s0 + js) * 3 + k];
-      else if (a.mu) vmu[js * 12 + k] = a.mu[(s0 + js) * 9 + (k - 3)];
+    if (a.v) {  // v (3) and mu (9) of the group's samples for the VJP tail (12 * Sv may
+                // exceed the block: 252 values at C = 3)
+      for (int t = tid; t < 12 * Sv; t += nthr) {
+        const int js = t / 12, k = t - 12 * js;
+        if (k < 3) vmu[js * 12 + k] = a.v[(s0 + js) * 3 + k];
+        else if (a.mu) vmu[js * 12 + k] = a.mu[(s0 + js) * 9 + (k - 3)];
+      }
     }
     // 3. the LDS-DMA writes of this wave have landed (an LDS-DMA is counted in vmcnt)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -388,13 +400,13 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
               float sum = v[0];
 #pragma unroll
               for (int jj = 1; jj < kSw; ++jj) sum += v[jj];
-              slabL[r0 * C + e] += sum;
+              slab_at(r0 * C + e) += sum;
             }
           } else {
             for (int e = lane; e < nn * C; e += 64) {
               float sum = col0[e];
               for (int jj = 1; jj < Sv; ++jj) sum += col0[jj * MC + e];
-              slabL[r0 * C + e] += sum;
+              slab_at(r0 * C + e) += sum;
             }
           }
         }

@@ -64,9 +64,9 @@ def test_backward_plans_fit_the_kernels(L):
                 assert p["lds_bytes"] <= (LDS_PER_CU if fallback else BWD_MAX_LDS)
                 groups = -(-n // p["samples_per_group"])
                 assert p["blocks"] == min(groups, 1024 if fallback else BWD_MAX_BLOCKS)
-                # workspace: the dF slabs, one per block; the LDS mode's slabs are sized for
-                # the chunk-major layout (16-element chunks, action_bwd.h kSlabChunk)
-                slab = (-(-MC // 16) * 16 if mode == 1 else MC)
+                # workspace: the dF slabs, one per block, sized for the chunk-major layout
+                # (16-element chunks, action_bwd.h kSlabChunk)
+                slab = -(-MC // 16) * 16
                 assert p["aux"] == (4 * p["blocks"] * slab if shared else 0)
                 assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
 

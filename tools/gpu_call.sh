@@ -84,7 +84,7 @@ for s in "$@"; do
         ${AB_C5:-base= pair=LV_TILE_BF16=1 alias=LV_TILE_BF16=4 both=LV_TILE_BF16=5 sw5=LV_TILE_SW=5 alias_sw5=LV_TILE_BF16=4,LV_TILE_SW=5}
       cat "$OUT/ab_c5.log" ;;
     ab-bwd)  # backward knob variants (AB_KNOBS, tools/bwd_reduce_ab.py) at AB_BATCHES
-      step ab_bwd 900 env AB_KNOBS="${AB_KNOBS:-LV_BWD_REDUCE=16,LV_BWD_REDUCE=3,LV_BWD_VARIANT=1,LV_BWD_REDUCE=3+LV_BWD_VARIANT=1,LV_BWD_REDUCE=16}" \
+      step ab_bwd 900 env AB_KNOBS="${AB_KNOBS:-LV_BWD_REDUCE=0,LV_BWD_REDUCE=16,LV_BWD_REDUCE=3,LV_BWD_VARIANT=1,LV_BWD_REDUCE=0}" \
         python tools/bwd_reduce_ab.py ${AB_BATCHES:-4096 512 65536}
       cat "$OUT/ab_bwd.log" ;;
     *)
