@@ -247,7 +247,8 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       const int e = lane + 64 * k;
       fv[k] = e < fcnt ? fsrc[e] : 0.f;
     }
-    for (int e = lane; e < fcnt; e += 64) slabL[rows_lo * C + e] = 0.f;  // this wave's rows
+    if constexpr (LOOP)
+      for (int e = lane; e < fcnt; e += 64) slabL[rows_lo * C + e] = 0.f;  // this wave's rows
     if constexpr (CT > 0) {
 #pragma unroll
       for (int k = 0; k < kFPer; ++k) {
@@ -384,7 +385,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
           gc += kdot<l>(u, f0);
         }
         if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
-        if constexpr (SHAREDF) {
+        if constexpr (SHAREDF && (LOOP || FM != kBwdFShared)) {
           // this degree's rows summed over the group's samples in sample order, added to
           // the block's slab (groups in order)
           wave_lds_sync();
@@ -413,9 +414,35 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       }
     });
     if constexpr (FM == kBwdFShared && !LOOP) {
-      // one group per block: this wave's slab rows are final -- write them now, ahead of
-      // the angle-gradient tail
-      write_slab_rows(a, slabL, rows_lo * C, fcnt, lane);
+      // one group per block: this wave's rows of the slab are the group's dF rows summed
+      // over its samples in sample order (the same sums as the looping path's per-degree
+      // slab adds, whose 0 + sum only differs in the sign of a zero, which the reduce's
+      // 0 + ... erases), taken once after the whole chain -- one LDS wait instead of one
+      // per degree -- and stored straight to the workspace, ahead of the angle tail
+      wave_lds_sync();
+      const float* t0 = reinterpret_cast<const float*>(stage_b);
+      constexpr int kSw = CT > 0 ? 64 / CT : 1;
+      const int g0 = rows_lo * C;
+      const bool full = CT > 0 && Sv == kSw && Sw == kSw;
+      float* ws = a.ws_F + (int64_t)blockIdx.x * (a.slab_chunked ? kSlabChunk : MC);
+      const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
+      for (int e = lane; e < fcnt; e += 64) {
+        const int g = g0 + e;
+        float sum;
+        if (full) {
+          float v[kSw];
+#pragma unroll
+          for (int jj = 0; jj < kSw; ++jj) v[jj] = t0[jj * MC + g];
+          sum = v[0];
+#pragma unroll
+          for (int jj = 1; jj < kSw; ++jj) sum += v[jj];
+        } else {
+          sum = t0[g];
+          for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
+        }
+        if (a.slab_chunked) ws[(g / kSlabChunk) * cstride + g % kSlabChunk] = sum;
+        else ws[g] = sum;
+      }
     }
     // angle gradients: sum over the C lanes of a sample (column order), then segments
     float* ap = apart + wave * 64 * 3;
