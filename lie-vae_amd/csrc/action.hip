@@ -440,7 +440,7 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 constexpr int64_t kBwdCUs = 256;  // MI355X compute units
 constexpr int kBwdReduceDefault = 3;  // LV_BWD_REDUCE default (see action_bwd_common)
-constexpr int kBwdVariantDefault = 0;  // LV_BWD_VARIANT default (kBwdVar* bits)
+constexpr int kBwdVariantDefault = kBwdVarJit;  // LV_BWD_VARIANT default (kBwdVar* bits; profiles/r04_bwd_reduce_ab.txt)
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
