@@ -13,6 +13,7 @@
 #   prof-driver  rocprofv3 --kernel-trace --stats of the driver-form bench
 #   train        bench_train.py config 3, bf16 channels-last, and the fp32 step
 #   rehearse     the N-rank rehearsal (two ranks sharing the GPU, gloo)
+#   pmc-bwd      PMC passes of the training direction (tools/gpu_pmc_bwd.sh)
 #   ab-c5        config-5 bf16 tile-option variants (AB_C5 overrides the list)
 #   ab-bwd       backward knob variants (AB_KNOBS, AB_BATCHES override)
 # Every GPU step runs under its own time limit; a fault, abort or time-limit kill ends
@@ -79,6 +80,8 @@ for s in "$@"; do
       grep '^{' "$OUT/train_f32.log" | cut -c1-240 ;;
     rehearse)
       step rehearse 600 bash tools/gpu_rehearse_ranks.sh ;;
+    pmc-bwd)
+      step pmc_bwd 900 bash tools/gpu_pmc_bwd.sh; cat "$OUT/pmc_bwd.log" ;;
     ab-c5)  # config-5 bf16 tile options (AB_C5 = the variant specs of tools/gpu_variants.sh)
       step ab_c5 900 bash tools/gpu_variants.sh "--lmax 20 --batch 8192 --dtype bf16 --sweep=65536" \
         ${AB_C5:-base= pair=LV_TILE_BF16=1 alias=LV_TILE_BF16=4 both=LV_TILE_BF16=5 sw5=LV_TILE_SW=5 alias_sw5=LV_TILE_BF16=4,LV_TILE_SW=5}

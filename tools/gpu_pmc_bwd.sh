@@ -15,6 +15,7 @@ for g in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS
 done
 python3 tools/pmc_summary.py "$OUT" action_bwd_tile > "$OUT/summary_bwd_tile.txt"
 python3 tools/pmc_summary.py "$OUT" action_bwd_reduce > "$OUT/summary_bwd_reduce.txt"
+python3 tools/pmc_summary.py "$OUT" action_fwd_tile > "$OUT/summary_fwd_tile.txt"
 find "$OUT" -name "*counter_collection.csv" -size +2M -delete
-cat "$OUT/summary_bwd_tile.txt" "$OUT/summary_bwd_reduce.txt"
+cat "$OUT/summary_bwd_tile.txt" "$OUT/summary_bwd_reduce.txt" "$OUT/summary_fwd_tile.txt"
 echo done
