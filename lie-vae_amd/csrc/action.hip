@@ -106,8 +106,10 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce2_kernel(const float* w
 // every slab b = t / 4, t / 4 + 256, ... (16-byte loads, all issued together), then the 256
 // partials of each quarter are added by a fixed-order halving tree.  Deterministic.
 __global__ __launch_bounds__(1024) void action_bwd_reduce3_kernel(const float* ws_F, float* gF, int64_t MC,
-                                                                  int nslab) {
+                                                                  int nslab, unsigned long long* stamps) {
   typedef float f4 __attribute__((ext_vector_type(4)));
+  unsigned long long* rst = stamps ? stamps + kStampBlocks * 16 * 8 + 2 * (int64_t)blockIdx.x : nullptr;
+  if (rst && threadIdx.x == 0) rst[0] = __builtin_amdgcn_s_memrealtime();
   __shared__ f4 part[256][4];
   const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
   const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)blockIdx.x * nslab * kSlabChunk) + q;
@@ -141,6 +143,7 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce3_kernel(const float* w
       const int64_t e = (int64_t)blockIdx.x * kSlabChunk + 4 * q + k;
       if (e < MC) gF[e] = r[k];
     }
+    if (rst) rst[1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -234,8 +237,21 @@ int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 #define LV_KNOB(name, dflt) env_int(name, dflt)
+// Phase-timestamp buffer of the timeline tool (LV_STAMPS=1, A/B build only): allocated once
+// on the first call, read back by lv_ab_stamps_copy.
+constexpr size_t kStampBytes = sizeof(unsigned long long) * ((size_t)kStampBlocks * 16 * 8 + 2 * 4096);
+unsigned long long* ab_stamps() {
+  static unsigned long long* p = nullptr;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    if (env_int("LV_STAMPS", 0) && hipMalloc(&p, kStampBytes) == hipSuccess) (void)hipMemset(p, 0, kStampBytes);
+  }
+  return p;
+}
 #else
 #define LV_KNOB(name, dflt) (dflt)
+inline unsigned long long* ab_stamps() { return nullptr; }
 #endif
 
 bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
@@ -405,6 +421,7 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   p.a.out = out;
   p.a.ang_out = ang_out;
   p.a.transpose = transpose ? 1 : 0;
+  p.a.stamps = ab_stamps();
   p.stream = stream;
   if (p.a.tflags && (reinterpret_cast<uintptr_t>(out) & 3)) {
     // the bf16-tile options write / read 4-byte words at tile offsets that are 4-byte
@@ -571,6 +588,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.a.slab_chunked = b.fmode != kBwdFSample && kEnvReduce == 3;
   static const int kEnvVariant = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
   p.a.variant = kEnvVariant;
+  p.a.stamps = ab_stamps();
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
   p.gx = b.gx;
   p.nseg = b.nseg;
@@ -586,7 +604,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // device-scope release fences -- ran 75 us per call at 4,096 and was dropped)
   if (p.a.slab_chunked) {
     hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
-                       (const float*)workspace, gF, MC, b.gx);
+                       (const float*)workspace, gF, MC, b.gx, p.a.stamps);
     LV_RETURN_LAUNCH("action_bwd_reduce3_kernel");
   }
   if (kEnvReduce == 8) {
@@ -708,5 +726,18 @@ int lv_wigner_d_fwd(const float* ang, float* D, int64_t n, int L, void* stream) 
     if (int e = kWigRun[l](p)) return e;
   return LV_OK;
 }
+
+#ifdef LV_AB_KNOBS
+// Timeline tool (A/B build): copy the phase-timestamp buffer to the host after a device
+// synchronise; returns the bytes copied (0 without LV_STAMPS=1).
+size_t lv_ab_stamps_copy(void* host, size_t bytes) {
+  unsigned long long* p = ab_stamps();
+  if (!p || !host) return 0;
+  bytes = std::min(bytes, kStampBytes);
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, p, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return bytes;
+}
+#endif
 
 }  // extern "C"

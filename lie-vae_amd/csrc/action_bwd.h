@@ -52,6 +52,7 @@ struct ActionBwdArgs {
   int prio;            // 2: group load + prologue at s_setprio 3, chain at 0 (A/B: 0 off)
   int slab_chunked;    // kBwdFShared slab layout: 0 [block][M*C], 1 [M*C/16][block][16]
   int variant;         // kernel variant bits (kBwdVar*)
+  unsigned long long* stamps;  // phase timestamps (A/B timeline tool; null in the product)
   int seg_lo[kMaxSeg + 1];
 };
 
@@ -279,6 +280,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
 
+  phase_stamp(a.stamps, wave, 0);
   for (int64_t g = blockIdx.x; g < a.groups; g += LOOP ? gridDim.x : a.groups) {
     const int64_t s0 = g * Sw;
     const int Sv = (int)min((int64_t)Sw, a.n - s0);
@@ -335,6 +337,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     // 3. the LDS-DMA writes of this wave have landed (an LDS-DMA is counted in vmcnt)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     block_sync_lds();
+    phase_stamp(a.stamps, wave, 1);
 
     if (a.prio >= 2) __builtin_amdgcn_s_setprio(0);
     float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
@@ -413,6 +416,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         }
       }
     });
+    phase_stamp(a.stamps, wave, 2);
     if constexpr (FM == kBwdFShared && !LOOP) {
       // one group per block: this wave's rows of the slab are the group's dF rows summed
       // over its samples in sample order (the same sums as the looping path's per-degree
@@ -444,6 +448,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         else ws[g] = sum;
       }
     }
+    phase_stamp(a.stamps, wave, 3);
     // angle gradients: sum over the C lanes of a sample (column order), then segments
     float* ap = apart + wave * 64 * 3;
     if (a.transpose) {
@@ -452,6 +457,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       ap[lane * 3 + 0] = ga; ap[lane * 3 + 1] = gb; ap[lane * 3 + 2] = gc;
     }
     block_sync_lds();
+    phase_stamp(a.stamps, wave, 4);
     if (tid < 3 * Sv) {
       const int js = tid / 3, i = tid - 3 * (tid / 3);
       const int nw = nthr >> 6;
@@ -464,7 +470,10 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       if (a.gang) a.gang[(s0 + js) * 3 + i] = r;
       if (a.v) trig[js * 3 + i] = r;  // the chains are done: the table is free
     }
-    if (!LOOP && SHAREDF && wave > 0) return;  // the tail below is wave 0's (tid < 3 * Sw)
+    if (!LOOP && SHAREDF && wave > 0) {  // the tail below is wave 0's (tid < 3 * Sw)
+      phase_stamp(a.stamps, wave, 5);
+      return;
+    }
     if (a.v) {  // fused path: exp -> ZYZ VJP of the group's samples (exp_eazyz_vjp_sample)
       if constexpr (!LOOP && SHAREDF) wave_lds_sync();  // wave 0 alone from here
       else block_sync_lds();
@@ -488,7 +497,10 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     }
     if constexpr (!SHAREDF)
       tile_flush<float, 1>(a.gF + s0 * MC, stage_b, mis, nbytes, tid, nthr);
-    if constexpr (!LOOP && SHAREDF) return;
+    if constexpr (!LOOP && SHAREDF) {
+      phase_stamp(a.stamps, wave, 5);
+      return;
+    }
     block_sync_lds();  // the next group overwrites the tile, the table and the partials
   }
   if constexpr (FM == kBwdFShared) write_slab_rows(a, slabL, rows_lo * C, fcnt, lane);

@@ -29,8 +29,18 @@ struct ActionArgs {
   int prio;             // tile kernel wave priority: 2 = prologue at s_setprio 3, chain at 0
                         // (default); A/B: 0 off, 1 flush at 3, 3 = 2 + flush at 2
   int tflags;           // tile kernel, bf16 tile with compile-time C (kTileBf16* bits)
+  unsigned long long* stamps;  // phase timestamps (A/B timeline tool; null in the product)
   int seg_lo[kMaxSeg + 1];
 };
+
+// Phase timestamps for tools/timeline.py (the A/B build's LV_STAMPS=1; the product passes
+// null): lane 0 of each wave writes the 100 MHz real-time counter at phase k, slot
+// [block][wave < 16][k < 8].
+constexpr int64_t kStampBlocks = 16384;
+__device__ __forceinline__ void phase_stamp(unsigned long long* st, int wave, int k) {
+  if (st && (threadIdx.x & 63) == 0 && blockIdx.x < kStampBlocks)
+    st[((int64_t)blockIdx.x * 16 + wave) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // bf16-tile options of the forward tile kernel (ActionArgs::tflags; compile-time C only):
 //   kTileBf16PairRows   rows i / i+1 leave each lane pair (c even, c+1) as one 4-byte LDS

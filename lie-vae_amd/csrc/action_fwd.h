@@ -306,6 +306,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   // FMA streams (tools/gpu_fwd_knobs.sh, profiles/r03_fwd_prio_ab.txt: batch 16,384
   // 20.96 -> 18.27 us, 65,536 63.6 -> 61.1, 262,144 256 -> 252; 4,096, where every block
   // starts at once, unchanged).  1 / 3: A/B variants with the flush raised.
+  phase_stamp(a.stamps, wave, 0);
   if (a.prio >= 2) __builtin_amdgcn_s_setprio(3);
   const int tid = (int)threadIdx.x;
   const bool task = tid < 3 * Sw;
@@ -370,6 +371,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     }
   }
   block_sync_lds();
+  phase_stamp(a.stamps, wave, 1);
 
   if (a.prio >= 2) __builtin_amdgcn_s_setprio(0);
   OutT* st_lane = reinterpret_cast<OutT*>(stage_b) + j * MC + c;
@@ -429,10 +431,13 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
       }
     }
   });
+  phase_stamp(a.stamps, wave, 2);
   block_sync_lds();
+  phase_stamp(a.stamps, wave, 3);
   if (a.prio == 1) __builtin_amdgcn_s_setprio(3);  // A/B: the flush ahead of other waves' chains
   else if (a.prio == 3) __builtin_amdgcn_s_setprio(2);
   tile_flush_rt<OutT>(gout, stage_b, mis, Sv * (int)MC * (int)sizeof(OutT), a.write_through);
+  phase_stamp(a.stamps, wave, 4);
 }
 
 template <int LT, int CT, bool FUSED, typename OutT>
