@@ -239,7 +239,7 @@ int env_int(const char* name, int dflt) {
 #define LV_KNOB(name, dflt) env_int(name, dflt)
 // Phase-timestamp buffer of the timeline tool (LV_STAMPS=1, A/B build only): allocated once
 // on the first call, read back by lv_ab_stamps_copy.
-constexpr size_t kStampBytes = sizeof(unsigned long long) * ((size_t)kStampBlocks * 16 * 8 + 2 * 4096);
+constexpr size_t kStampBytes = sizeof(unsigned long long) * ((size_t)kStampDegBase + kStampDegBlocks * 16 * 24);
 unsigned long long* ab_stamps() {
   static unsigned long long* p = nullptr;
   static bool tried = false;

@@ -414,6 +414,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
             }
           }
         }
+        if (a.stamps) degree_stamp(a.stamps, wave, l);
       }
     });
     phase_stamp(a.stamps, wave, 2);
@@ -430,22 +431,37 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       const bool full = CT > 0 && Sv == kSw && Sw == kSw;
       float* ws = a.ws_F + (int64_t)blockIdx.x * (a.slab_chunked ? kSlabChunk : MC);
       const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
-      for (int e = lane; e < fcnt; e += 64) {
-        const int g = g0 + e;
-        float sum;
-        if (full) {
-          float v[kSw];
-#pragma unroll
-          for (int jj = 0; jj < kSw; ++jj) v[jj] = t0[jj * MC + g];
-          sum = v[0];
-#pragma unroll
-          for (int jj = 1; jj < kSw; ++jj) sum += v[jj];
-        } else {
-          sum = t0[g];
-          for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
-        }
+      auto put = [&](int g, float sum) {
         if (a.slab_chunked) ws[(g / kSlabChunk) * cstride + g % kSlabChunk] = sum;
         else ws[g] = sum;
+      };
+      if (full) {
+        // four elements per lane per pass, all their LDS loads issued before any sum or
+        // global store (one LDS round trip per pass instead of one per element)
+        constexpr int kU = 4;
+        for (int e0 = lane; e0 < fcnt; e0 += kU * 64) {
+          float v[kU][kSw];
+#pragma unroll
+          for (int u = 0; u < kU; ++u) {
+            const int g = g0 + min(e0 + 64 * u, fcnt - 1);  // clamped: in-range reads
+#pragma unroll
+            for (int jj = 0; jj < kSw; ++jj) v[u][jj] = t0[jj * MC + g];
+          }
+#pragma unroll
+          for (int u = 0; u < kU; ++u) {
+            float sum = v[u][0];
+#pragma unroll
+            for (int jj = 1; jj < kSw; ++jj) sum += v[u][jj];
+            if (e0 + 64 * u < fcnt) put(g0 + e0 + 64 * u, sum);
+          }
+        }
+      } else {
+        for (int e = lane; e < fcnt; e += 64) {
+          const int g = g0 + e;
+          float sum = t0[g];
+          for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
+          put(g, sum);
+        }
       }
     }
     phase_stamp(a.stamps, wave, 3);

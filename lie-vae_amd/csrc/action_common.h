@@ -41,6 +41,14 @@ __device__ __forceinline__ void phase_stamp(unsigned long long* st, int wave, in
   if (st && (threadIdx.x & 63) == 0 && blockIdx.x < kStampBlocks)
     st[((int64_t)blockIdx.x * 16 + wave) * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
+// ... and at the end of each degree l of the chain, slot [block < 2048][wave][l < 24] after
+// the phase slots and the reduce kernel's 2 x 4096 (per-degree cost calibration).
+constexpr int64_t kStampDegBlocks = 2048;
+constexpr int64_t kStampDegBase = kStampBlocks * 16 * 8 + 2 * 4096;
+__device__ __forceinline__ void degree_stamp(unsigned long long* st, int wave, int l) {
+  if (st && (threadIdx.x & 63) == 0 && blockIdx.x < kStampDegBlocks)
+    st[kStampDegBase + ((int64_t)blockIdx.x * 16 + wave) * 24 + l] = __builtin_amdgcn_s_memrealtime();
+}
 
 // bf16-tile options of the forward tile kernel (ActionArgs::tflags; compile-time C only):
 //   kTileBf16PairRows   rows i / i+1 leave each lane pair (c even, c+1) as one 4-byte LDS

@@ -324,10 +324,16 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     const int e = lane + 64 * k;
     fv[k] = e < fcnt ? fsrc[e] : 0.f;
   }
+  if (a.stamps) {  // A/B timeline: when this wave's loads (v; spectrum slice) have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    phase_stamp(a.stamps, wave, 5);
+  }
   if (task) {
     float c1[3], s1[3];
     lane_angles<FUSED, MAYMU>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
+    if (a.stamps) phase_stamp(a.stamps, wave, 6);
     trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
+    if (a.stamps) phase_stamp(a.stamps, wave, 7);
   }
   if constexpr (FG) {
   } else if constexpr (CT > 0) {
@@ -429,6 +435,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
           d += C;
         });
       }
+      if (a.stamps) degree_stamp(a.stamps, wave, l);
     }
   });
   phase_stamp(a.stamps, wave, 2);

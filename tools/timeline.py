@@ -22,17 +22,39 @@ KB = 16384  # kStampBlocks
 TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 
-def stamps(lib):
-    n = KB * 16 * 8 + 2 * 4096
+DEG_BASE, DEG_BLOCKS = KB * 16 * 8 + 2 * 4096, 2048
+
+
+def stamps(lib, with_deg=False):
+    n = DEG_BASE + DEG_BLOCKS * 16 * 24
     buf = np.zeros(n, dtype=np.uint64)
     fn = lib.lv_ab_stamps_copy
     fn.restype, fn.argtypes = ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_size_t]
     got = fn(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
     assert got == buf.nbytes, "LV_STAMPS=1 and the A/B library (LIEVAE_HIP_LIB) are required"
-    return buf[: KB * 16 * 8].reshape(KB, 16, 8).astype(np.int64), buf[KB * 16 * 8:].reshape(4096, 2).astype(np.int64)
+    out = (buf[: KB * 16 * 8].reshape(KB, 16, 8).astype(np.int64),
+           buf[KB * 16 * 8: DEG_BASE].reshape(4096, 2).astype(np.int64))
+    if with_deg:
+        out = out + (buf[DEG_BASE:].reshape(DEG_BLOCKS, 16, 24).astype(np.int64),)
+    return out
 
 
-def report(name, st, nblk, nwave, phases, red=None, nred=0):
+def degree_costs(name, st, deg, nblk, seg):
+    """Median time per degree (us): stamp at the end of degree l minus the end of the
+    wave's previous degree (phase-1 stamp for its first)."""
+    nb = min(nblk, DEG_BLOCKS)
+    res = {}
+    for w in range(len(seg) - 1):
+        prev = st[:nb, w, 1]
+        for l in range(seg[w], seg[w + 1]):
+            d = (deg[:nb, w, l] - prev) * TICK_US
+            res[l] = (w, float(np.median(d)))
+            prev = deg[:nb, w, l]
+    print(f"  {name} per-degree median us: " + " ".join(f"l{l}(w{w}):{t:.3f}" for l, (w, t) in sorted(res.items())))
+    return res
+
+
+def report(name, st, nblk, nwave, phases, red=None, nred=0, extra=None):
     s = st[:nblk, :nwave, :]
     t0 = s[:, :, 0][s[:, :, 0] > 0].min()
     print(f"== {name}: {nblk} blocks x {nwave} waves")
@@ -49,6 +71,12 @@ def report(name, st, nblk, nwave, phases, red=None, nred=0):
           f"{np.percentile(start, 90):6.2f} {start.max():6.2f} us")
     print(f"  block finish p10/50/90/max {np.percentile(end, 10):6.2f} {np.median(end):6.2f} "
           f"{np.percentile(end, 90):6.2f} {end.max():6.2f} us")
+    if extra:
+        for k, nm in extra:
+            d = us(s[:, :, k] - s[:, :, 0])
+            ok = s[:, :, k] > 0
+            print(f"  {nm}: median " + " ".join(f"{np.median(d[:, w][ok[:, w]]):5.2f}" if ok[:, w].any() else "  -  "
+                                            for w in range(nwave)) + " us after wave start")
     first = [us(np.median(s[:, w, 1] - t0)) for w in range(nwave)]
     print("  median time of phase 1 end per wave (from grid start): " + " ".join(f"{x:5.2f}" for x in first))
     if red is not None and nred:
@@ -79,11 +107,13 @@ def main():
     if which in ("fwd", "both"):
         for _ in range(R):
             assert lib.lv_fused_exp_action_fwd(None, P(v), P(F), 0, P(out), code, P(ang), B, L, C, 0, None) == 0
-        st, _ = stamps(lib)
+        st, _, deg = stamps(lib, True)
         print(f"plan: blocks {plan[1]} segments {plan[2]} lds {plan[4]} seg_lo "
               f"{[plan[7 + k] for k in range(plan[2] + 1)]}")
         report(f"fused forward B={B} l={L} {dt}", st, min(plan[1], KB), plan[2],
-               ["start", "prologue", "chain", "barrier", "flush"])
+               ["start", "prologue", "chain", "barrier", "flush"],
+               extra=[(5, "loads landed"), (6, "exp->ZYZ done (wave 0)"), (7, "multiples done (wave 0)")])
+        degree_costs("forward", st, deg, plan[1], [plan[7 + k] for k in range(plan[2] + 1)])
     if which in ("bwd", "both"):
         lib.lv_fused_exp_action_fwd(None, P(v), P(F), 0, P(out), _lib.LV_DTYPE_F32, P(ang), B, L, C, 0, None)
         gout = torch.randn(B, M, C, generator=g).to(dev)
@@ -95,10 +125,11 @@ def main():
         for _ in range(R):
             assert lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0, P(ws), wsb,
                                            None) == 0
-        st, red = stamps(lib)
+        st, red, deg = stamps(lib, True)
         print(f"bwd plan: blocks {bp[1]} segments {bp[2]} lds {bp[4]} seg_lo {[bp[7 + k] for k in range(bp[2] + 1)]}")
         report(f"group-action backward B={B} l={L}", st, min(bp[1], KB), bp[2],
                ["start", "load+prologue", "chain", "slab", "angle-sync", "end"], red, (M * C + 15) // 16)
+        degree_costs("backward", st, deg, bp[1], [bp[7 + k] for k in range(bp[2] + 1)])
 
 
 if __name__ == "__main__":
