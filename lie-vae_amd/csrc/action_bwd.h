@@ -256,7 +256,16 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         const int e = lane + 64 * k;
         if (e < fcnt) Fw[e] = fv[k];
       }
-      for (int e = lane + 64 * kFPer; e < fcnt; e += 64) Fw[e] = fsrc[e];
+      // the rest (long segments at high l: up to 1,000 values) in passes of 8 loads per
+      // lane issued together, not one dependent global load per iteration
+      for (int e0 = lane + 64 * kFPer; e0 < fcnt; e0 += 8 * 64) {
+        float t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t8[u] = e0 + 64 * u < fcnt ? fsrc[e0 + 64 * u] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + 64 * u < fcnt) Fw[e0 + 64 * u] = t8[u];
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < kFPer; ++k) {

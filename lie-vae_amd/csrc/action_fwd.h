@@ -360,7 +360,16 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
         const int e = lane + 64 * k;
         if (e < fcnt) Fw[e] = fv[k];
       }
-      for (int e = lane + 64 * kFPer; e < fcnt; e += 64) Fw[e] = fsrc[e];
+      // the rest (long segments at high l: up to 1,000 values) in passes of 8 loads per
+      // lane issued together, not one dependent global load per iteration
+      for (int e0 = lane + 64 * kFPer; e0 < fcnt; e0 += 8 * 64) {
+        float t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t8[u] = e0 + 64 * u < fcnt ? fsrc[e0 + 64 * u] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + 64 * u < fcnt) Fw[e0 + 64 * u] = t8[u];
+      }
     }
   } else {
 #pragma unroll
@@ -447,9 +456,9 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   phase_stamp(a.stamps, wave, 4);
 }
 
-template <int LT, int CT, bool FUSED, typename OutT>
+template <int LT, int CT, bool FUSED, typename OutT, bool MAYMU = true>
 __global__ __launch_bounds__(512) void action_fwd_tile_kernel(ActionArgs a) {
-  fwd_tile_body<LT, CT, FUSED, OutT>(a, blockIdx.x);
+  fwd_tile_body<LT, CT, FUSED, OutT, MAYMU>(a, blockIdx.x);
 }
 
 
@@ -509,7 +518,15 @@ template <int LT>
 template <int CT>
 void FwdLauncher<LT>::launch_tile(FwdLaunch& p, bool bf16) {
   const dim3 grid(p.gx), block(64 * p.gy);
-  if (p.fused) {
+  if (p.fused && CT > 0 && !p.a.mu) {
+    // no mean rotation (the metric path, z = exp(v)): the instantiation without the fp64
+    // mu prologue -- 1,660 -> ~700 instructions ahead of the first barrier at l = 10, so
+    // fewer cold instruction-cache lines on every block's critical path
+    if (bf16)
+      hipLaunchKernelGGL((action_fwd_tile_kernel<LT, CT, true, __hip_bfloat16, false>), grid, block, p.lds, p.stream, p.a);
+    else
+      hipLaunchKernelGGL((action_fwd_tile_kernel<LT, CT, true, float, false>), grid, block, p.lds, p.stream, p.a);
+  } else if (p.fused) {
     if (bf16)
       hipLaunchKernelGGL((action_fwd_tile_kernel<LT, CT, true, __hip_bfloat16>), grid, block, p.lds, p.stream, p.a);
     else
