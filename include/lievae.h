@@ -148,8 +148,11 @@ size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F);
  * slab in the workspace -- the large-tile fallback), [1] grid blocks,
  * [2] degree segments, [3] threads per block, [4] dynamic LDS bytes per block,
  * [5] samples per block group, [6] forward: write-through stores / backward: workspace
- * bytes, [7..] segment boundaries seg_lo[0..segments] (then -1).  n > 0. */
-#define LV_PLAN_LEN 24
+ * bytes, [7..23] segment boundaries seg_lo[0..segments] (then -1), [24..39] the degree
+ * set of wave k (bit l = degree l; 0 past the last wave): the kernels run these sets --
+ * contiguous ranges seg_lo where a kernel stages per-wave spectrum rows, cost-balanced
+ * sets otherwise.  n > 0. */
+#define LV_PLAN_LEN 40
 int lv_action_fwd_plan(int fused, int64_t F_batch_stride, int out_dtype, int64_t n, int L, int C,
                        int64_t* plan);
 int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* plan);

@@ -194,6 +194,37 @@ inline int plan_segments(int L, int nseg, double P, bool bwd, int* seg_lo) {
   return nseg;
 }
 
+// Degree sets of the waves, balanced by cost (LPT: degrees in decreasing cost -- decreasing
+// l -- each to the least loaded wave, ties to the lowest index).  Contiguous ranges cannot
+// balance the high degrees (in-kernel per-degree timings, profiles/r04_timeline_*.txt:
+// backward l = 10 segments [0,6) [6,8) [8,10) [10] ran 3.9 / 4.0 / 5.2 / 3.6 us, and every
+// wave of a block waits at the barrier for the slowest).  Each degree also carries a fixed
+// cost (multiples reads, spectrum column, LDS round trips): kDegFixed, fitted to the same
+// timings.
+constexpr double kDegFixedFwd = 40.0, kDegFixedBwd = 30.0;
+inline double degree_cost_sched(int l, bool bwd) {
+  return (bwd ? kDegFixedBwd : kDegFixedFwd) + degree_cost(l, bwd);
+}
+inline void balance_masks(int L, int nseg, bool bwd, unsigned* masks) {
+  double load[kMaxSeg];
+  for (int k = 0; k < nseg; ++k) { load[k] = 0.0; masks[k] = 0u; }
+  for (int l = L; l >= 0; --l) {
+    int best = 0;
+    for (int k = 1; k < nseg; ++k)
+      if (load[k] < load[best]) best = k;
+    masks[best] |= 1u << l;
+    load[best] += degree_cost_sched(l, bwd);
+  }
+  for (int k = nseg; k < kMaxSeg; ++k) masks[k] = 0u;
+}
+inline void contiguous_masks(const int* seg_lo, int nseg, unsigned* masks) {
+  for (int k = 0; k < kMaxSeg; ++k) {
+    masks[k] = 0u;
+    if (k < nseg)
+      for (int l = seg_lo[k]; l < seg_lo[k + 1]; ++l) masks[k] |= 1u << l;
+  }
+}
+
 // Segments so that the grid has ~2.7 waves per SIMD (1024 SIMDs on MI355X; measured
 // best at batch 4096, l = 10: 4 segments), but never more ranges than pay for their
 // duplicated prologue.
@@ -224,7 +255,6 @@ constexpr double kTileSegCostLarge = 560.0;  // ... many groups (>= kTileManyGro
 constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
 constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
-constexpr int kTileBf16Default = 0;  // bf16 tile options in the product (kTileBf16* bits)
 
 // A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
 // LV_*_NSEG force segment counts, LV_BWD_FGLOBAL forces the backward's global-spectrum
@@ -259,17 +289,12 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
   static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
   static const int kEnvPrio = LV_KNOB("LV_TILE_PRIO", 2);      // wave priority phases (ActionArgs)
-  // bf16 tile with compile-time C: kTileBf16* options and the samples per block (A/B knobs
-  // LV_TILE_BF16 = option bits, LV_TILE_SW = samples per block)
-  static const int kEnvBf16 = LV_KNOB("LV_TILE_BF16", kTileBf16Default);
+  // samples per block with compile-time C (A/B knob LV_TILE_SW)
   static const int kEnvSw = LV_KNOB("LV_TILE_SW", 0);
   if (!kEnvTile) return false;
   ActionArgs& a = p.a;
-  const bool bt = out_bytes == 2 && a.C == kTileFastC;
   int Sw = 64 / a.C;
-  a.tflags = bt ? kEnvBf16 : 0;
   if (a.C == kTileFastC && kEnvSw >= 2 && kEnvSw < Sw) Sw = kEnvSw;
-  if (Sw < 2) a.tflags &= ~kTileBf16SpecAlias;
   const int64_t groups = (a.n + Sw - 1) / Sw;
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
@@ -280,17 +305,19 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
   if (3 * Sw > 64 * nseg || nseg > 8) return false;
   plan_segments(L, nseg, kTilePrologue, false, a.seg_lo);
+  // compile-time C: cost-balanced degree sets; run-time C keeps the contiguous ranges
+  // (its spectrum slices are per-wave row ranges)
+  static const int kEnvContig = LV_KNOB("LV_SEG_CONTIG", 0);  // A/B: contiguous ranges everywhere
+  if (a.C == kTileFastC && !kEnvContig) balance_masks(L, nseg, false, a.seg_mask);
+  else contiguous_masks(a.seg_lo, nseg, a.seg_mask);
   // spectrum in LDS: C = kTileFastC -> the whole (M, C) once, row-major; other C ->
   // per-wave column-major slices below kTileFGlobalMinL, global memory from there
   int fp = 0;
   if (a.C != kTileFastC && L < kTileFGlobalMinL)
     for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(a.seg_lo[k], a.seg_lo[k + 1]) * a.C);
   a.fpitch = (fp + 3) & ~3;
-  // (C = kTileFastC with fp32 output: the spectrum sits in the tile's last sample slot;
-  // bf16 with kTileBf16SpecAlias: in its last two)
-  const size_t fl = a.C == kTileFastC
-                        ? (out_bytes == 4 || (a.tflags & kTileBf16SpecAlias) ? 0 : (size_t)a.MC)
-                        : (size_t)nseg * a.fpitch;
+  // (C = kTileFastC with fp32 output: the spectrum sits in the tile's last sample slot)
+  const size_t fl = a.C == kTileFastC ? (out_bytes == 4 ? 0 : (size_t)a.MC) : (size_t)nseg * a.fpitch;
   const size_t trig = (size_t)Sw * (6 * ((L + 1 + 3) & ~3) + 4);  // TrigLds<L>::kRow per sample
   const size_t lds = (size_t)tile_stage_bytes(Sw, a.MC, out_bytes) + sizeof(float) * (fl + trig);
   if (lds > kTileMaxLds || groups > 0x7fffffff) return false;
@@ -354,6 +381,7 @@ int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C
   const int nseg = kEnvFwdNseg > 0 ? std::min(kEnvFwdNseg, std::min(L + 1, kMaxSeg))
                                    : choose_nseg(n, p.a.Sw, L, P, false);
   plan_segments(L, nseg, P, false, p.a.seg_lo);
+  contiguous_masks(p.a.seg_lo, nseg, p.a.seg_mask);  // (reported by the plan query only)
   const int64_t gx = (n + (int64_t)p.a.Sw * kWavesPerBlock - 1) / ((int64_t)p.a.Sw * kWavesPerBlock);
   LV_CHECK_ARG(gx <= 0x7fffffff, "batch too large");
   p.gx = (int)gx;
@@ -423,12 +451,6 @@ int action_fwd_common(bool fused, const float* ang, const float* mu, const float
   p.a.transpose = transpose ? 1 : 0;
   p.a.stamps = ab_stamps();
   p.stream = stream;
-  if (p.a.tflags && (reinterpret_cast<uintptr_t>(out) & 3)) {
-    // the bf16-tile options write / read 4-byte words at tile offsets that are 4-byte
-    // aligned only when the output is (2-byte aligned views take the plain tile)
-    if (p.a.tflags & kTileBf16SpecAlias) p.lds += sizeof(float) * (size_t)p.a.MC;
-    p.a.tflags = 0;
-  }
   return dispatch_L<FwdLauncher>(L, p);
 }
 
@@ -470,6 +492,7 @@ struct BwdPlan {
   int Sw, nseg, gx, fpitch, fmode;
   int64_t groups;
   int seg_lo[kMaxSeg + 1];
+  unsigned seg_mask[kMaxSeg];
   size_t lds, ws;
 };
 
@@ -496,14 +519,22 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
       if (3 * Sw > 64 * nseg || nseg > 8) continue;
       plan_segments(L, nseg, kTilePrologue, true, b.seg_lo);
+      // the run-time-C kernel with the spectrum in LDS stages per-wave row ranges: contiguous
+      // degree sets; every other kernel takes cost-balanced sets (compile-time C stages the
+      // whole spectrum once per block)
+      const bool ct = C == kTileFastC && fmode == kBwdFShared;
+      static const int kEnvContig = LV_KNOB("LV_SEG_CONTIG", 0);  // A/B: contiguous ranges everywhere
+      if ((fmode == kBwdFShared && !ct) || kEnvContig) contiguous_masks(b.seg_lo, nseg, b.seg_mask);
+      else balance_masks(L, nseg, true, b.seg_mask);
       int fp = 0;
-      if (fmode == kBwdFShared)
+      if (fmode == kBwdFShared && !ct)
         for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(b.seg_lo[k], b.seg_lo[k + 1]) * C);
       b.fpitch = (fp + 3) & ~3;
+      const size_t fregion = ct ? (size_t)((MC + 3) & ~3) : (size_t)nseg * b.fpitch;
       const size_t lds = (size_t)tile_stage_bytes(Sw, MC, 4) +
                          sizeof(float) * ((size_t)bwd_trig_floats(Sw, L) + (size_t)nseg * 64 * 3 +
                                           (fmode == kBwdFShared ? (size_t)MC : 0) +
-                                          (size_t)nseg * b.fpitch + 12 * (size_t)Sw);
+                                          fregion + 12 * (size_t)Sw);
       if (lds > cap) continue;
       b.Sw = Sw;
       b.nseg = nseg;
@@ -537,7 +568,7 @@ bool plan_bwd_cached(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
 }  // namespace lv
 
 using namespace lv;
-static_assert(7 + kMaxSeg + 1 == LV_PLAN_LEN, "plan layout (include/lievae.h)");
+static_assert(7 + kMaxSeg + 1 + kMaxSeg == LV_PLAN_LEN, "plan layout (include/lievae.h)");
 
 namespace {
 int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
@@ -590,6 +621,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.a.variant = kEnvVariant;
   p.a.stamps = ab_stamps();
   for (int k = 0; k <= b.nseg; ++k) p.a.seg_lo[k] = b.seg_lo[k];
+  for (int k = 0; k < kMaxSeg; ++k) p.a.seg_mask[k] = b.seg_mask[k];
   p.gx = b.gx;
   p.nseg = b.nseg;
   p.fmode = b.fmode;
@@ -694,6 +726,7 @@ int lv_action_fwd_plan(int fused, int64_t F_batch_stride, int out_dtype, int64_t
   plan[5] = p.a.Sw;
   plan[6] = p.a.write_through;
   for (int k = 0; k <= kMaxSeg; ++k) plan[7 + k] = k <= p.gy ? p.a.seg_lo[k] : -1;
+  for (int k = 0; k < kMaxSeg; ++k) plan[8 + kMaxSeg + k] = k < p.gy ? (int64_t)p.a.seg_mask[k] : 0;
   return LV_OK;
 }
 
@@ -712,6 +745,7 @@ int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* pla
   plan[5] = b.Sw;
   plan[6] = (int64_t)b.ws;
   for (int k = 0; k <= kMaxSeg; ++k) plan[7 + k] = k <= b.nseg ? b.seg_lo[k] : -1;
+  for (int k = 0; k < kMaxSeg; ++k) plan[8 + kMaxSeg + k] = k < b.nseg ? (int64_t)b.seg_mask[k] : 0;
   return LV_OK;
 }
 

@@ -53,7 +53,8 @@ struct ActionBwdArgs {
   int slab_chunked;    // kBwdFShared slab layout: 0 [block][M*C], 1 [M*C/16][block][16]
   int variant;         // kernel variant bits (kBwdVar*)
   unsigned long long* stamps;  // phase timestamps (A/B timeline tool; null in the product)
-  int seg_lo[kMaxSeg + 1];
+  int seg_lo[kMaxSeg + 1];      // contiguous degree ranges (run-time-C kernel, LDS spectrum)
+  unsigned seg_mask[kMaxSeg];   // degree set of wave k (bit l = degree l)
 };
 
 // Chunk-major dF slabs (slab_chunked): element e of block b at
@@ -215,11 +216,18 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   const int tid = (int)threadIdx.x, nthr = (int)blockDim.x;
   const int j = lane / C;
   const int c = lane - j * C;
+  // this wave's degrees: a bit set (balanced by cost in the planner); the run-time-C kernel
+  // with the spectrum in LDS keeps contiguous ranges [lo, hi) for its column-major slices
+  const unsigned dmask = a.seg_mask[wave];
   const int lo = a.seg_lo[wave], hi = a.seg_lo[wave + 1];
   const int rows_lo = lo * lo;
   const int frows = fseg_rows(lo, hi);
+  auto each_degree = [&](auto&& fn) {  // the wave's degrees, ascending (scalar loop)
+    for (unsigned m = dmask; m; m &= m - 1) fn(__builtin_ctz(m));
+  };
   const int stage_bytes = tile_stage_bytes(Sw, MC, 4);
-  // LDS: [gout / dF tile][multiples table][angle partials][dF slab (shared F)][F slices]
+  // LDS: [gout / dF tile][multiples table][angle partials][dF slab (shared F)][spectrum:
+  //      CT > 0 the whole (M, C) row-major, else per-wave column-major slices]
   //      [fused path: the group's v (and mu), Sw * 12 floats]
   float* trig = lds + (stage_bytes >> 2);
   float* apart = trig + bwd_trig_floats(Sw, LT);               // [nseg][64][3]
@@ -234,57 +242,65 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     }
     return slabL[g];
   };
-  float* Fw = apart + (nthr >> 6) * 64 * 3 + (FM == kBwdFShared ? (int)MC : 0) + wave * a.fpitch;
-  // spectrum slice (shared F): once per block
-  constexpr int kFPer = 6;
-  const int fcnt = SHAREDF ? (hi * hi - rows_lo) * C : 0;
-  const float* fsrc = a.F + rows_lo * C;
+  float* const Fbase = apart + (nthr >> 6) * 64 * 3 + (FM == kBwdFShared ? (int)MC : 0);
+  const int fsize = CT > 0 ? (((int)MC + 3) & ~3) : (nthr >> 6) * a.fpitch;
+  float* Fw = Fbase + (CT > 0 ? 0 : wave * a.fpitch);
+  // spectrum (shared F): once per block -- CT > 0: element e = tid + k * nthr of the whole
+  // (M, C) by every thread, loads issued together; else this wave's column-major slice
+  constexpr int kFPer = CT > 0 ? ((LT + 1) * (LT + 1) * (CT > 0 ? CT : 1) + 255) / 256 : 6;
+  constexpr int kFPerCap = kFPer < 16 ? kFPer : 16;
+  const int fcnt = SHAREDF ? (CT > 0 ? (int)MC : (hi * hi - rows_lo) * C) : 0;
+  const int fstr = CT > 0 ? nthr : 64;
+  const int fbase = CT > 0 ? tid : lane;
+  const float* fsrc = a.F + (CT > 0 ? 0 : rows_lo * C);
   if constexpr (GSLAB) {
-    for (int e = lane; e < fcnt; e += 64) slab_at(rows_lo * C + e) = 0.f;  // this wave's rows
+    each_degree([&](int l) {  // this wave's rows
+      for (int e = lane; e < (2 * l + 1) * C; e += 64) slab_at(l * l * C + e) = 0.f;
+    });
   } else if constexpr (SHAREDF) {
-    float fv[kFPer];
+    float fv[kFPerCap];
 #pragma unroll
-    for (int k = 0; k < kFPer; ++k) {
-      const int e = lane + 64 * k;
+    for (int k = 0; k < kFPerCap; ++k) {
+      const int e = fbase + fstr * k;
       fv[k] = e < fcnt ? fsrc[e] : 0.f;
     }
     if constexpr (LOOP)
-      for (int e = lane; e < fcnt; e += 64) slabL[rows_lo * C + e] = 0.f;  // this wave's rows
+      each_degree([&](int l) {  // this wave's rows
+        for (int e = lane; e < (2 * l + 1) * C; e += 64) slabL[l * l * C + e] = 0.f;
+      });
     if constexpr (CT > 0) {
 #pragma unroll
-      for (int k = 0; k < kFPer; ++k) {
-        const int e = lane + 64 * k;
+      for (int k = 0; k < kFPerCap; ++k) {
+        const int e = fbase + fstr * k;
         if (e < fcnt) Fw[e] = fv[k];
       }
-      // the rest (long segments at high l: up to 1,000 values) in passes of 8 loads per
-      // lane issued together, not one dependent global load per iteration
-      for (int e0 = lane + 64 * kFPer; e0 < fcnt; e0 += 8 * 64) {
+      for (int e0 = fbase + fstr * kFPerCap; e0 < fcnt; e0 += 8 * fstr) {
         float t8[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t8[u] = e0 + 64 * u < fcnt ? fsrc[e0 + 64 * u] : 0.f;
+        for (int u = 0; u < 8; ++u) t8[u] = e0 + fstr * u < fcnt ? fsrc[e0 + fstr * u] : 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-          if (e0 + 64 * u < fcnt) Fw[e0 + 64 * u] = t8[u];
+          if (e0 + fstr * u < fcnt) Fw[e0 + fstr * u] = t8[u];
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < kFPer; ++k) {
+      for (int k = 0; k < kFPerCap; ++k) {
         const int e = lane + 64 * k;
         if (e < fcnt) {
           const int r = e / C, cc2 = e - r * C;
           Fw[cc2 * frows + r] = fv[k];
         }
       }
-      for (int e = lane + 64 * kFPer; e < fcnt; e += 64) {
+      for (int e = lane + 64 * kFPerCap; e < fcnt; e += 64) {
         const int r = e / C, cc2 = e - r * C;
         Fw[cc2 * frows + r] = fsrc[e];
       }
     }
   }
   // fused path: the exp -> ZYZ VJP's inputs, loaded by the prologue threads so that the
-  // tail does not wait on global loads (after the last spectrum slice)
-  float* vmu = apart + (nthr >> 6) * 64 * 3 + (FM == kBwdFShared ? (int)MC : 0) + (nthr >> 6) * a.fpitch;
-  const float* Fl = GSLAB ? a.F + c : (CT > 0 ? Fw + c - rows_lo * C : Fw + c * frows - rows_lo);
+  // tail does not wait on global loads (after the spectrum)
+  float* vmu = Fbase + fsize;
+  const float* Fl = GSLAB ? a.F + c : (CT > 0 ? Fw + c : Fw + c * frows - rows_lo);
   const int fstep = (GSLAB || CT > 0) ? C : 1;
   const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
@@ -355,7 +371,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     float ga = 0.f, gb = 0.f, gc = 0.f;
     sfor<LT + 1>([&](auto Lc) {
       constexpr int l = LV_CV(Lc);
-      if (l >= lo && l < hi) {
+      if ((dmask >> l) & 1u) {
         constexpr int nn = 2 * l + 1;
         constexpr int r0 = l * l;
         // live arrays kept to three or four of 2l+1: the spectrum column and G are
@@ -436,7 +452,6 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       wave_lds_sync();
       const float* t0 = reinterpret_cast<const float*>(stage_b);
       constexpr int kSw = CT > 0 ? 64 / CT : 1;
-      const int g0 = rows_lo * C;
       const bool full = CT > 0 && Sv == kSw && Sw == kSw;
       float* ws = a.ws_F + (int64_t)blockIdx.x * (a.slab_chunked ? kSlabChunk : MC);
       const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
@@ -444,34 +459,37 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         if (a.slab_chunked) ws[(g / kSlabChunk) * cstride + g % kSlabChunk] = sum;
         else ws[g] = sum;
       };
-      if (full) {
-        // four elements per lane per pass, all their LDS loads issued before any sum or
-        // global store (one LDS round trip per pass instead of one per element)
-        constexpr int kU = 4;
-        for (int e0 = lane; e0 < fcnt; e0 += kU * 64) {
-          float v[kU][kSw];
+      each_degree([&](int l) {
+        const int g0 = l * l * C, cnt = (2 * l + 1) * C;
+        if (full) {
+          // four elements per lane per pass, all their LDS loads issued before any sum or
+          // global store (one LDS round trip per pass instead of one per element)
+          constexpr int kU = 4;
+          for (int e0 = lane; e0 < cnt; e0 += kU * 64) {
+            float v[kU][kSw];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) {
-            const int g = g0 + min(e0 + 64 * u, fcnt - 1);  // clamped: in-range reads
+            for (int u = 0; u < kU; ++u) {
+              const int g = g0 + min(e0 + 64 * u, cnt - 1);  // clamped: in-range reads
 #pragma unroll
-            for (int jj = 0; jj < kSw; ++jj) v[u][jj] = t0[jj * MC + g];
+              for (int jj = 0; jj < kSw; ++jj) v[u][jj] = t0[jj * MC + g];
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+              float sum = v[u][0];
+#pragma unroll
+              for (int jj = 1; jj < kSw; ++jj) sum += v[u][jj];
+              if (e0 + 64 * u < cnt) put(g0 + e0 + 64 * u, sum);
+            }
           }
-#pragma unroll
-          for (int u = 0; u < kU; ++u) {
-            float sum = v[u][0];
-#pragma unroll
-            for (int jj = 1; jj < kSw; ++jj) sum += v[u][jj];
-            if (e0 + 64 * u < fcnt) put(g0 + e0 + 64 * u, sum);
+        } else {
+          for (int e = lane; e < cnt; e += 64) {
+            const int g = g0 + e;
+            float sum = t0[g];
+            for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
+            put(g, sum);
           }
         }
-      } else {
-        for (int e = lane; e < fcnt; e += 64) {
-          const int g = g0 + e;
-          float sum = t0[g];
-          for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
-          put(g, sum);
-        }
-      }
+      });
     }
     phase_stamp(a.stamps, wave, 3);
     // angle gradients: sum over the C lanes of a sample (column order), then segments
@@ -528,7 +546,8 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     }
     block_sync_lds();  // the next group overwrites the tile, the table and the partials
   }
-  if constexpr (FM == kBwdFShared) write_slab_rows(a, slabL, rows_lo * C, fcnt, lane);
+  if constexpr (FM == kBwdFShared)
+    each_degree([&](int l) { write_slab_rows(a, slabL, l * l * C, (2 * l + 1) * C, lane); });
 }
 
 // Slab count per block of action_bwd_reduce_kernel (defined in action.hip).

@@ -28,9 +28,9 @@ struct ActionArgs {
   int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores, 2 = plain (A/B)
   int prio;             // tile kernel wave priority: 2 = prologue at s_setprio 3, chain at 0
                         // (default); A/B: 0 off, 1 flush at 3, 3 = 2 + flush at 2
-  int tflags;           // tile kernel, bf16 tile with compile-time C (kTileBf16* bits)
   unsigned long long* stamps;  // phase timestamps (A/B timeline tool; null in the product)
-  int seg_lo[kMaxSeg + 1];
+  int seg_lo[kMaxSeg + 1];      // non-tile kernel / run-time-C tile: contiguous degree ranges
+  unsigned seg_mask[kMaxSeg];   // tile kernel: degree set of wave k (bit l = degree l)
 };
 
 // Phase timestamps for tools/timeline.py (the A/B build's LV_STAMPS=1; the product passes
@@ -50,16 +50,6 @@ __device__ __forceinline__ void degree_stamp(unsigned long long* st, int wave, i
     st[kStampDegBase + ((int64_t)blockIdx.x * 16 + wave) * 24 + l] = __builtin_amdgcn_s_memrealtime();
 }
 
-// bf16-tile options of the forward tile kernel (ActionArgs::tflags; compile-time C only):
-//   kTileBf16PairRows   rows i / i+1 leave each lane pair (c even, c+1) as one 4-byte LDS
-//                       write per lane (DPP swap + v_cvt_pk_bf16_f32) instead of two
-//                       2-byte writes that share a dword
-//   kTileBf16SpecAlias  the fp32 spectrum lives in the tile's last two sample slots: degree
-//                       l's (2l+1)·C values split in two halves over the two slots' rows of
-//                       degree l (degree-local: only the wave of degree l touches them, and
-//                       it reads them before it writes its own rows there); no separate
-//                       M·C·4-byte spectrum area
-constexpr int kTileBf16PairRows = 1, kTileBf16SpecAlias = 4;
 
 // ---- fused-prologue maths (per lane, registers).
 

@@ -270,15 +270,17 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   // rows, so the slot is free to be overwritten; the block saves M*C*4 bytes of LDS
   // (l = 10: 35.7 -> 30.9 KB, 4 -> 5 blocks per CU).
   constexpr bool FT = CT > 0 && std::is_same_v<OutT, float>;
-  constexpr bool BT = CT > 0 && !FT;  // bf16 tile, compile-time C: a.tflags options
-  const bool alias = BT && (a.tflags & kTileBf16SpecAlias);
   const int C = CT > 0 ? CT : a.C;
   const int Sw = a.Sw;  // 64 / C, or fewer (plan: LDS per block vs blocks per CU)
   const int64_t MC = CT > 0 ? (int64_t)(LT + 1) * (LT + 1) * CT : a.MC;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
+  const int tid = (int)threadIdx.x, nthr = (int)blockDim.x;
   const int j = lane / C;
   const int c = lane - j * C;
+  // this wave's degrees: a bit set (compile-time C: any set the planner balanced by cost);
+  // run-time C keeps contiguous ranges [lo, hi) for its column-major spectrum slices
+  const unsigned dmask = a.seg_mask[wave];
   const int lo = a.seg_lo[wave], hi = a.seg_lo[wave + 1];
   const int rows_lo = lo * lo;
   const int frows = fseg_rows(lo, hi);
@@ -290,15 +292,10 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   OutT* gout = reinterpret_cast<OutT*>(a.out) + s0 * MC;
   const int mis = (int)(reinterpret_cast<uintptr_t>(gout) & 15);
   char* stage_b = reinterpret_cast<char*>(lds) + mis;  // LDS addr = global addr (mod 16)
-  // spectrum in LDS: CT > 0 the whole (M, C) row-major (each wave fills its rows; FT: in
-  // the tile's last sample slot), else per-wave column-major slices of a.fpitch floats
+  // spectrum in LDS: CT > 0 the whole (M, C) row-major, staged by all threads of the block
+  // (FT: in the tile's last sample slot), else per-wave column-major slices of a.fpitch
   float* const Fall = FT ? reinterpret_cast<float*>(stage_b) + (Sw - 1) * MC : trig + Sw * kRow;
-  float* Fw = Fall + (CT > 0 ? rows_lo * C : wave * a.fpitch);
-  // alias (bf16 tile): degree l's spectrum values e < (2l+1)·C/2 at slot Sw-2, rows of degree
-  // l, as fp32 (the rows' bytes hold exactly half the degree's fp32 values), the rest at
-  // slot Sw-1; a.Sw, the tile base and MC keep every such address 4-byte aligned (host plan)
-  char* const ahalf0 = stage_b + (int64_t)(Sw - 2) * MC * 2;
-  char* const ahalf1 = stage_b + (int64_t)(Sw - 1) * MC * 2;
+  float* Fw = Fall + (CT > 0 ? 0 : wave * a.fpitch);
   // 1. prologue task (sample jt, slot q); the host guarantees 3*Sw <= blockDim.x
   // Wave priority (a.prio, the plan's default 2): the prologue (v / mu loads, exp -> ZYZ,
   // multiples, spectrum staging) issues at s_setprio 3 and the chain at 0, so on a CU that
@@ -308,23 +305,28 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   // starts at once, unchanged).  1 / 3: A/B variants with the flush raised.
   phase_stamp(a.stamps, wave, 0);
   if (a.prio >= 2) __builtin_amdgcn_s_setprio(3);
-  const int tid = (int)threadIdx.x;
   const bool task = tid < 3 * Sw;
   const int jt = tid / 3, q = tid - 3 * (tid / 3);
   const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
   LaneIn in;
   if (task) lane_load<FUSED, MAYMU>(a, st, in);
-  // 2. this wave's spectrum slice: loads now, LDS writes after the prologue maths
-  constexpr int kFPer = FG ? 1 : 6;
-  float fv[kFPer];
-  const int fcnt = FG ? 0 : (hi * hi - rows_lo) * C;
-  const float* fsrc = a.F + rows_lo * C;
+  // 2. spectrum staging: every load issued now (before the prologue maths), the LDS writes
+  //    after it.  CT > 0: element e = tid + k * nthr of the whole (M, C) spectrum, at most
+  //    kFPer per thread for the smallest block the plan makes (2 waves), a batched loop
+  //    beyond; else this wave's column-major slice.
+  constexpr int kFPer = FG ? 1 : (CT > 0 ? ((LT + 1) * (LT + 1) * (CT > 0 ? CT : 1) + 127) / 128 : 6);
+  constexpr int kFPerCap = kFPer < 18 ? kFPer : 18;
+  float fv[kFPerCap];
+  const int fcnt = FG ? 0 : (CT > 0 ? (int)MC : (hi * hi - rows_lo) * C);
+  const int fstr = CT > 0 ? nthr : 64;
+  const int fbase = CT > 0 ? tid : lane;
+  const float* fsrc = a.F + (CT > 0 ? 0 : rows_lo * C);
 #pragma unroll
-  for (int k = 0; k < kFPer; ++k) {
-    const int e = lane + 64 * k;
+  for (int k = 0; k < kFPerCap; ++k) {
+    const int e = fbase + fstr * k;
     fv[k] = e < fcnt ? fsrc[e] : 0.f;
   }
-  if (a.stamps) {  // A/B timeline: when this wave's loads (v; spectrum slice) have landed
+  if (a.stamps) {  // A/B timeline: when this wave's loads (v; spectrum) have landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     phase_stamp(a.stamps, wave, 5);
   }
@@ -337,50 +339,29 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   }
   if constexpr (FG) {
   } else if constexpr (CT > 0) {
-    if (alias) {
-      // the wave's degrees [lo, hi): value e of degree l (e = k·C + c, k < 2l+1) goes to
-      // half (e >= (2l+1)·C/2) at byte 2·(l²·C) + 4·(e mod half) of that half's slot
-      auto put = [&](int e, float v) {
-        const int g = rows_lo * C + e;            // global spectrum index
-        int l = lo;
-        while ((l + 1) * (l + 1) * C <= g) ++l;   // degree of g (short: l in [lo, hi))
-        const int e0 = g - l * l * C, half = (2 * l + 1) * C / 2;
-        char* dst = (e0 < half ? ahalf0 : ahalf1) + 2 * l * l * C + 4 * (e0 < half ? e0 : e0 - half);
-        *reinterpret_cast<float*>(dst) = v;
-      };
 #pragma unroll
-      for (int k = 0; k < kFPer; ++k) {
-        const int e = lane + 64 * k;
-        if (e < fcnt) put(e, fv[k]);
-      }
-      for (int e = lane + 64 * kFPer; e < fcnt; e += 64) put(e, fsrc[e]);
-    } else {
+    for (int k = 0; k < kFPerCap; ++k) {
+      const int e = fbase + fstr * k;
+      if (e < fcnt) Fw[e] = fv[k];
+    }
+    for (int e0 = fbase + fstr * kFPerCap; e0 < fcnt; e0 += 8 * fstr) {
+      float t8[8];
 #pragma unroll
-      for (int k = 0; k < kFPer; ++k) {
-        const int e = lane + 64 * k;
-        if (e < fcnt) Fw[e] = fv[k];
-      }
-      // the rest (long segments at high l: up to 1,000 values) in passes of 8 loads per
-      // lane issued together, not one dependent global load per iteration
-      for (int e0 = lane + 64 * kFPer; e0 < fcnt; e0 += 8 * 64) {
-        float t8[8];
+      for (int u = 0; u < 8; ++u) t8[u] = e0 + fstr * u < fcnt ? fsrc[e0 + fstr * u] : 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t8[u] = e0 + 64 * u < fcnt ? fsrc[e0 + 64 * u] : 0.f;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (e0 + 64 * u < fcnt) Fw[e0 + 64 * u] = t8[u];
-      }
+      for (int u = 0; u < 8; ++u)
+        if (e0 + fstr * u < fcnt) Fw[e0 + fstr * u] = t8[u];
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < kFPer; ++k) {
+    for (int k = 0; k < kFPerCap; ++k) {
       const int e = lane + 64 * k;
       if (e < fcnt) {
         const int r = e / C, cc = e - r * C;
         Fw[cc * frows + r] = fv[k];
       }
     }
-    for (int e = lane + 64 * kFPer; e < fcnt; e += 64) {
+    for (int e = lane + 64 * kFPerCap; e < fcnt; e += 64) {
       const int r = e / C, cc = e - r * C;
       Fw[cc * frows + r] = fsrc[e];
     }
@@ -397,47 +378,17 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
 
   sfor<LT + 1>([&](auto Lc) {
     constexpr int l = LV_CV(Lc);
-    if (l >= lo && l < hi) {
+    if ((dmask >> l) & 1u) {
       constexpr int nn = 2 * l + 1;
       constexpr int r0 = l * l;
       float x[nn], y[nn];
-      if (BT && alias) {
-        // (k, c) -> value e = k·C + c of the degree; rows below the middle one sit in the
-        // first half, above it in the second, the middle row splits at c = C/2
-        constexpr int half = nn * (CT > 0 ? CT : 1) / 2;
-        const float* h0 = reinterpret_cast<const float*>(ahalf0 + 2 * r0 * C) + c;
-        const float* h1 = reinterpret_cast<const float*>(ahalf1 + 2 * r0 * C) + c - half;
-        sfor<nn>([&](auto K) {
-          constexpr int k = LV_CV(K);
-          if constexpr (k < l) x[k] = h0[k * C];
-          else if constexpr (k > l) x[k] = h1[k * C];
-          else x[k] = (c < C / 2) ? h0[k * C] : h1[k * C];
-        });
-      } else {
-        sfor<nn>([&](auto K) { x[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * fstep]; });
-      }
+      sfor<nn>([&](auto K) { x[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * fstep]; });
       xrot_lds<l, 2, LT>(tj, x, y);
       jmul<l>(y, x);
       xrot_lds<l, 1, LT>(tj, x, y);
       jmul<l>(y, x);
       xrot_lds<l, 0, LT>(tj, x, y);
-      if (BT && (a.tflags & kTileBf16PairRows)) {
-        // rows (i, i+1) of the lane pair (c even, c+1): the even lane writes row i, cols
-        // (c, c+1), the odd lane row i+1, cols (c-1, c) -- one dword each; the last
-        // (unpaired) row as before
-        const bool odd = (c & 1) != 0;
-        OutT* d = st_lane + r0 * C + (odd ? C - 1 : 0);
-        sfor<nn / 2>([&](auto P) {
-          constexpr int i = 2 * LV_CV(P);
-          const float recv = dpp_swap_adjacent(odd ? y[i] : y[i + 1]);
-          __hip_bfloat162 h;  // the same RNE conversion as tile_cvt, two at once
-          h.x = __float2bfloat16(odd ? recv : y[i]);
-          h.y = __float2bfloat16(odd ? y[i + 1] : recv);
-          if (active) *reinterpret_cast<__hip_bfloat162*>(d) = h;
-          d += 2 * C;
-        });
-        if (active) st_lane[(r0 + nn - 1) * C] = tile_cvt(y[nn - 1], (OutT*)nullptr);
-      } else if (active) {
+      if (active) {
         OutT* d = st_lane + r0 * C;
         sfor<nn>([&](auto I) {
           d[0] = tile_cvt(y[LV_CV(I)], (OutT*)nullptr);

@@ -139,7 +139,7 @@ def call(name, *args):
         raise LieVaeHipError(f"{name} failed ({rc}): {last_error()}")
 
 
-PLAN_LEN = 24  # LV_PLAN_LEN
+PLAN_LEN = 40  # LV_PLAN_LEN
 PLAN_FIELDS = ("tile", "blocks", "segments", "threads", "lds_bytes", "samples_per_group", "aux")
 
 
@@ -149,7 +149,8 @@ def plan(kind, *args):
     buf = (ctypes.c_int64 * PLAN_LEN)()
     call("lv_action_fwd_plan" if kind == "fwd" else "lv_group_action_bwd_plan", *args, buf)
     d = dict(zip(PLAN_FIELDS, buf[:7]))
-    d["seg_lo"] = [x for x in buf[7:] if x >= 0]
+    d["seg_lo"] = [x for x in buf[7:24] if x >= 0]
+    d["seg_mask"] = list(buf[24:24 + d["segments"]])
     return d
 
 

@@ -19,6 +19,15 @@ def _check_segments(p, L):
     assert len(seg) == p["segments"] + 1
     assert seg[0] == 0 and seg[-1] == L + 1
     assert all(a < b for a, b in zip(seg, seg[1:])), seg
+    # the degree sets the kernels run: one non-empty set per wave, together a partition of
+    # 0..L (each degree's rows belong to exactly one wave)
+    masks = p["seg_mask"]
+    assert len(masks) == p["segments"] and all(m > 0 for m in masks), masks
+    acc = 0
+    for m in masks:
+        assert acc & m == 0, masks
+        acc |= m
+    assert acc == (1 << (L + 1)) - 1, masks
 
 
 @pytest.mark.parametrize("L", list(range(0, 21)))

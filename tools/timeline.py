@@ -39,14 +39,14 @@ def stamps(lib, with_deg=False):
     return out
 
 
-def degree_costs(name, st, deg, nblk, seg):
+def degree_costs(name, st, deg, nblk, masks):
     """Median time per degree (us): stamp at the end of degree l minus the end of the
     wave's previous degree (phase-1 stamp for its first)."""
     nb = min(nblk, DEG_BLOCKS)
     res = {}
-    for w in range(len(seg) - 1):
+    for w, m in enumerate(masks):
         prev = st[:nb, w, 1]
-        for l in range(seg[w], seg[w + 1]):
+        for l in [b for b in range(24) if (m >> b) & 1]:
             d = (deg[:nb, w, l] - prev) * TICK_US
             res[l] = (w, float(np.median(d)))
             prev = deg[:nb, w, l]
@@ -101,35 +101,35 @@ def main():
     odt = torch.bfloat16 if dt == "bf16" else torch.float32
     out = torch.empty(B, M, C, device=dev, dtype=odt)
     ang = torch.empty(B, 3, device=dev)
-    plan = (ctypes.c_int64 * 24)()
+    plan = (ctypes.c_int64 * 40)()
     code = _lib.LV_DTYPE_BF16 if dt == "bf16" else _lib.LV_DTYPE_F32
     assert lib.lv_action_fwd_plan(1, 0, code, B, L, C, plan) == 0
     if which in ("fwd", "both"):
         for _ in range(R):
             assert lib.lv_fused_exp_action_fwd(None, P(v), P(F), 0, P(out), code, P(ang), B, L, C, 0, None) == 0
         st, _, deg = stamps(lib, True)
-        print(f"plan: blocks {plan[1]} segments {plan[2]} lds {plan[4]} seg_lo "
-              f"{[plan[7 + k] for k in range(plan[2] + 1)]}")
+        print(f"plan: blocks {plan[1]} segments {plan[2]} lds {plan[4]} degree sets "
+              f"{[bin(plan[24 + k]) for k in range(plan[2])]}")
         report(f"fused forward B={B} l={L} {dt}", st, min(plan[1], KB), plan[2],
                ["start", "prologue", "chain", "barrier", "flush"],
                extra=[(5, "loads landed"), (6, "exp->ZYZ done (wave 0)"), (7, "multiples done (wave 0)")])
-        degree_costs("forward", st, deg, plan[1], [plan[7 + k] for k in range(plan[2] + 1)])
+        degree_costs("forward", st, deg, plan[1], [plan[24 + k] for k in range(plan[2])])
     if which in ("bwd", "both"):
         lib.lv_fused_exp_action_fwd(None, P(v), P(F), 0, P(out), _lib.LV_DTYPE_F32, P(ang), B, L, C, 0, None)
         gout = torch.randn(B, M, C, generator=g).to(dev)
         gang, gF = torch.empty(B, 3, device=dev), torch.empty(M, C, device=dev)
         wsb = lib.lv_group_action_bwd_workspace(B, L, C, 1)
         ws = torch.zeros(max(wsb, 1), device=dev, dtype=torch.uint8)
-        bp = (ctypes.c_int64 * 24)()
+        bp = (ctypes.c_int64 * 40)()
         assert lib.lv_group_action_bwd_plan(B, L, C, 1, bp) == 0
         for _ in range(R):
             assert lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0, P(ws), wsb,
                                            None) == 0
         st, red, deg = stamps(lib, True)
-        print(f"bwd plan: blocks {bp[1]} segments {bp[2]} lds {bp[4]} seg_lo {[bp[7 + k] for k in range(bp[2] + 1)]}")
+        print(f"bwd plan: blocks {bp[1]} segments {bp[2]} lds {bp[4]} degree sets {[bin(bp[24 + k]) for k in range(bp[2])]}")
         report(f"group-action backward B={B} l={L}", st, min(bp[1], KB), bp[2],
                ["start", "load+prologue", "chain", "slab", "angle-sync", "end"], red, (M * C + 15) // 16)
-        degree_costs("backward", st, deg, bp[1], [bp[7 + k] for k in range(bp[2] + 1)])
+        degree_costs("backward", st, deg, bp[1], [bp[24 + k] for k in range(bp[2])])
 
 
 if __name__ == "__main__":
