@@ -338,18 +338,11 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     // 2. prologue task (sample jt, slot q): sincos, multiples of slot q
     if (task) {
       const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
-      float cc[3], ss[3], c1[3], s1[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) sincosf(a.ang[st * 3 + i], &ss[i], &cc[i]);
-      if (a.transpose) {
-        c1[0] = cc[2]; s1[0] = -ss[2];
-        c1[1] = cc[1]; s1[1] = -ss[1];
-        c1[2] = cc[0]; s1[2] = -ss[0];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { c1[i] = cc[i]; s1[i] = ss[i]; }
-      }
-      trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
+      // only this slot's angle (transpose: slot q takes angle 2 - q, sine negated)
+      float cq, sq;
+      sincosf(a.ang[st * 3 + (a.transpose ? 2 - q : q)], &sq, &cq);
+      if (a.transpose) sq = -sq;
+      trig_row_fill1<LT>(trig + jt * kRow, cq, sq, q, LT);
     }
     if (a.v) {  // v (3) and mu (9) of the group's samples for the VJP tail (12 * Sv may
                 // exceed the block: 252 values at C = 3)

@@ -110,6 +110,31 @@ __device__ __forceinline__ void trig_row_fill(float* tj, const float c1[3], cons
   });
 }
 
+// The same for one slot whose (cos, sin) the caller already picked (bitwise equal).
+template <int LT>
+__device__ __forceinline__ void trig_row_fill1(float* tj, float cq, float sq, int q, int upto) {
+  constexpr int TP = TrigLds<LT>::TP;
+  float* tc = tj + 2 * q * TP;
+  float* ts = tc + TP;
+  tc[0] = 1.f;
+  ts[0] = 0.f;
+  float cf = cq, sf = sq;
+  sfor<LT + 1>([&](auto F) {
+    constexpr int f = LV_CV(F);
+    if constexpr (f >= 1) {
+      if (f <= upto) {
+        if constexpr (f >= 2) {
+          const float cn = fmaf(cf, cq, -(sf * sq));
+          sf = fmaf(sf, cq, cf * sq);
+          cf = cn;
+        }
+        tc[f] = cf;
+        ts[f] = sf;
+      }
+    }
+  });
+}
+
 // y = X_l(θ_A) x with the multiples read from an LDS row (bitwise equal to xrot): the
 // l+1 needed (cos, sin) pairs are fetched with 16-byte reads right before the product,
 // so they occupy registers only while it runs.

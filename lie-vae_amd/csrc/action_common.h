@@ -105,8 +105,10 @@ __device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], f
   const float qk = k == 0 ? qt[0] : (k == 1 ? qt[1] : (k == 2 ? qt[2] : qt[3]));
   constexpr float eps = 2.5e-7f;
   const float qk2 = qk * qk;
-  const float d = sqrtf(qk2 + eps);
-  const float sc = copysignf(best / d, qk);
+  // d = sqrt(qk^2 + eps), best / d as reciprocal-square-root products (<= 2 ulp)
+  const float rd = rsqrtf(qk2 + eps);
+  const float d = (qk2 + eps) * rd;
+  const float sc = copysignf(best * rd, qk);
 #pragma unroll
   for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
   const float oms = eps * (1.f - 2.f * qk2 - eps) / (qk2 + eps);  // 1 - |q_ref|^2
@@ -116,7 +118,7 @@ __device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], f
   if (omc < kDelta) { omc = kDelta; opc = 2.f - kDelta; }
   else if (opc < kDelta) { opc = kDelta; omc = 2.f - kDelta; }
   c1[1] = omc <= opc ? 1.f - omc : opc - 1.f;
-  s1[1] = sqrtf(omc * opc);
+  s1[1] = __builtin_amdgcn_sqrtf(omc * opc);  // v_sqrt_f32 (1 ulp)
   auto dir = [](float y, float x, float& c, float& s) {
     const float r2 = x * x + y * y;
     if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
@@ -130,6 +132,54 @@ __device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], f
   };
   dir(qr[1] * qr[2] - qr[0] * qr[3], qr[0] * qr[2] + qr[1] * qr[3], c1[0], s1[0]);
   dir(qr[0] * qr[3] + qr[1] * qr[2], qr[1] * qr[3] - qr[0] * qr[2], c1[2], s1[2]);
+}
+
+// One slot of exp_to_zyz_trig (angle index ai: 0 = alpha, 1 = beta, 2 = gamma), the same
+// arithmetic: each prologue thread of the tile kernel fills one slot's multiples, so it
+// computes that slot's (cos, sin) only (and the quaternion, for ang_out).
+__device__ __forceinline__ void exp_to_zyz_slot(const float v[3], int ai, float& c, float& s, float qr[4]) {
+  const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const float inv = rsqrtf(vv);  // NaN downstream at v = 0, as the reference
+  const float th = vv * inv;
+  float sh, ch;
+  sincosf(0.5f * th, &sh, &ch);
+  const float m = -sh * inv;
+  const float qt[4] = {v[0] * m, v[1] * m, v[2] * m, ch};
+  int k = 0;
+  float best = fabsf(qt[0]);
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (fabsf(qt[i]) > best) { best = fabsf(qt[i]); k = i; }
+  const float qk = k == 0 ? qt[0] : (k == 1 ? qt[1] : (k == 2 ? qt[2] : qt[3]));
+  constexpr float eps = 2.5e-7f;
+  const float qk2 = qk * qk;
+  const float rd = rsqrtf(qk2 + eps);
+  const float d = (qk2 + eps) * rd;
+  const float sc = copysignf(best * rd, qk);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
+  if (ai == 1) {
+    const float oms = eps * (1.f - 2.f * qk2 - eps) / (qk2 + eps);  // 1 - |q_ref|^2
+    float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
+    float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
+    constexpr float kDelta = 1.f - kEazyzHi;
+    if (omc < kDelta) { omc = kDelta; opc = 2.f - kDelta; }
+    else if (opc < kDelta) { opc = kDelta; omc = 2.f - kDelta; }
+    c = omc <= opc ? 1.f - omc : opc - 1.f;
+    s = __builtin_amdgcn_sqrtf(omc * opc);
+  } else {
+    const float y = ai == 0 ? qr[1] * qr[2] - qr[0] * qr[3] : qr[0] * qr[3] + qr[1] * qr[2];
+    const float x = ai == 0 ? qr[0] * qr[2] + qr[1] * qr[3] : qr[1] * qr[3] - qr[0] * qr[2];
+    const float r2 = x * x + y * y;
+    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
+      c = signbit(x) ? -1.f : 1.f;
+      s = 0.f;
+    } else {
+      const float r = rsqrtf(r2);
+      c = x * r;
+      s = y * r;
+    }
+  }
 }
 
 // General mean (z = mu @ exp(v)): the reference's op sequence (rodrigues, matmul, trace

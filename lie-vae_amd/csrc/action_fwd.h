@@ -331,10 +331,27 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     phase_stamp(a.stamps, wave, 5);
   }
   if (task) {
-    float c1[3], s1[3];
-    lane_angles<FUSED, MAYMU>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
+    float cq, sq;
+    if constexpr (FUSED && !MAYMU) {
+      // z = exp(v): this thread's slot only (transpose: slot q takes angle 2 - q, sine negated)
+      float qr[4];
+      exp_to_zyz_slot(in.v, a.transpose ? 2 - q : q, cq, sq, qr);
+      if (a.transpose) sq = -sq;
+      if (a.ang_out && jt < Sv && q == 0) {
+        float ang[3];
+        quat_to_eazyz_fwd(qr, ang);
+        a.ang_out[st * 3 + 0] = ang[0];
+        a.ang_out[st * 3 + 1] = ang[1];
+        a.ang_out[st * 3 + 2] = ang[2];
+      }
+    } else {
+      float c1[3], s1[3];
+      lane_angles<FUSED, MAYMU>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
+      cq = q == 0 ? c1[0] : (q == 1 ? c1[1] : c1[2]);
+      sq = q == 0 ? s1[0] : (q == 1 ? s1[1] : s1[2]);
+    }
     if (a.stamps) phase_stamp(a.stamps, wave, 6);
-    trig_row_fill<LT>(trig + jt * kRow, c1, s1, q, LT);
+    trig_row_fill1<LT>(trig + jt * kRow, cq, sq, q, LT);
     if (a.stamps) phase_stamp(a.stamps, wave, 7);
   }
   if constexpr (FG) {
