@@ -134,15 +134,43 @@ __device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], f
   dir(qr[0] * qr[3] + qr[1] * qr[2], qr[1] * qr[3] - qr[0] * qr[2], c1[2], s1[2]);
 }
 
-// One slot of exp_to_zyz_trig (angle index ai: 0 = alpha, 1 = beta, 2 = gamma), the same
-// arithmetic: each prologue thread of the tile kernel fills one slot's multiples, so it
-// computes that slot's (cos, sin) only (and the quaternion, for ang_out).
+// sin and cos of x as straight-line code: Cody-Waite reduction by pi/2 (three-part fp32
+// constant, FMA) into [-pi/4, pi/4], minimax polynomials (the Cephes sinf / cosf
+// coefficients) and the quadrant by k & 3; <= 1.6 ulp for |x| <= 1e5 (checked against fp64
+// on 430k points).  Larger |x| (a rotation vector beyond 2e5 rad) and NaN take sincosf on a
+// cold branch.  The library's sincosf inlines its large-argument reduction in the middle of
+// the code, and in the tile kernels' prologue -- one serial chain per (sample, slot) that
+// every wave of the block waits for -- the jumps around it land on cold instruction-cache
+// lines.
+__device__ __forceinline__ void lv_sincos(float x, float& s, float& c) {
+  const float k = rintf(x * 0.63661977236758134f);
+  float r = fmaf(k, -1.5707963705062866f, x);
+  r = fmaf(k, 4.371138828673793e-08f, r);
+  r = fmaf(k, 1.7151245100058819e-15f, r);
+  const float r2 = r * r;
+  const float ps = fmaf(r2, fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f) * r2;
+  const float sn = fmaf(r, ps, r);
+  const float pc = fmaf(r2, fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f);
+  const float cs = fmaf(r2 * r2, pc, fmaf(r2, -0.5f, 1.f));
+  const int q = (int)k & 3;
+  s = (q & 1) ? cs : sn;
+  c = (q & 1) ? sn : cs;
+  if (q == 1 || q == 2) c = -c;
+  if (q >= 2) s = -s;
+  if (__builtin_expect(!(fabsf(x) <= 1.0e5f), 0)) sincosf(x, &s, &c);
+}
+
+// One slot of exp_to_zyz_trig (angle index ai: 0 = alpha, 1 = beta, 2 = gamma) as
+// straight-line code (selects, no divergent branches): each prologue thread of the tile
+// kernel fills one slot's multiples, so it computes that slot's (cos, sin) only (and the
+// quaternion, for ang_out).  Same formulas as exp_to_zyz_trig; lv_sincos for the half
+// angle and rsqrt products for the divisions (<= 2 ulp).
 __device__ __forceinline__ void exp_to_zyz_slot(const float v[3], int ai, float& c, float& s, float qr[4]) {
   const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
   const float inv = rsqrtf(vv);  // NaN downstream at v = 0, as the reference
   const float th = vv * inv;
   float sh, ch;
-  sincosf(0.5f * th, &sh, &ch);
+  lv_sincos(0.5f * th, sh, ch);
   const float m = -sh * inv;
   const float qt[4] = {v[0] * m, v[1] * m, v[2] * m, ch};
   int k = 0;
@@ -158,28 +186,25 @@ __device__ __forceinline__ void exp_to_zyz_slot(const float v[3], int ai, float&
   const float sc = copysignf(best * rd, qk);
 #pragma unroll
   for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
-  if (ai == 1) {
-    const float oms = eps * (1.f - 2.f * qk2 - eps) / (qk2 + eps);  // 1 - |q_ref|^2
-    float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
-    float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
-    constexpr float kDelta = 1.f - kEazyzHi;
-    if (omc < kDelta) { omc = kDelta; opc = 2.f - kDelta; }
-    else if (opc < kDelta) { opc = kDelta; omc = 2.f - kDelta; }
-    c = omc <= opc ? 1.f - omc : opc - 1.f;
-    s = __builtin_amdgcn_sqrtf(omc * opc);
-  } else {
-    const float y = ai == 0 ? qr[1] * qr[2] - qr[0] * qr[3] : qr[0] * qr[3] + qr[1] * qr[2];
-    const float x = ai == 0 ? qr[0] * qr[2] + qr[1] * qr[3] : qr[1] * qr[3] - qr[0] * qr[2];
-    const float r2 = x * x + y * y;
-    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
-      c = signbit(x) ? -1.f : 1.f;
-      s = 0.f;
-    } else {
-      const float r = rsqrtf(r2);
-      c = x * r;
-      s = y * r;
-    }
-  }
+  // beta: cos from the "one-minus" forms, clamp to +-(1 - 1e-6) mirrored
+  const float oms = eps * (1.f - 2.f * qk2 - eps) * (rd * rd);       // 1 - |q_ref|^2
+  float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
+  float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
+  constexpr float kDelta = 1.f - kEazyzHi;
+  const bool clo = omc < kDelta, chi = !clo && opc < kDelta;
+  omc = clo ? kDelta : (chi ? 2.f - kDelta : omc);
+  opc = clo ? 2.f - kDelta : (chi ? kDelta : opc);
+  const float cb = omc <= opc ? 1.f - omc : opc - 1.f;
+  const float sb = __builtin_amdgcn_sqrtf(omc * opc);
+  // alpha / gamma: the direction of (x, y), atan2(+-0, +-0) in {0, +-pi} mirrored
+  const float y = ai == 0 ? qr[1] * qr[2] - qr[0] * qr[3] : qr[0] * qr[3] + qr[1] * qr[2];
+  const float x = ai == 0 ? qr[0] * qr[2] + qr[1] * qr[3] : qr[1] * qr[3] - qr[0] * qr[2];
+  const float r2 = x * x + y * y;
+  const float rr = rsqrtf(r2);
+  const float cd = r2 == 0.f ? (signbit(x) ? -1.f : 1.f) : x * rr;
+  const float sd = r2 == 0.f ? 0.f : y * rr;
+  c = ai == 1 ? cb : cd;
+  s = ai == 1 ? sb : sd;
 }
 
 // General mean (z = mu @ exp(v)): the reference's op sequence (rodrigues, matmul, trace
