@@ -32,6 +32,9 @@ namespace lv {
 // so bitwise equal to kBwdFShared for the same plan.
 constexpr int kBwdFSample = 0, kBwdFShared = 1, kBwdFSharedGlobal = 2;
 constexpr int kBwdVarJit = 1;  // ActionBwdArgs::variant: row-pair reads of F and G (wide kernel)
+// one-group blocks' post-chain slab pass (A/B): flat element list over the wave's degrees
+// (else one pass set per degree), and write-through (sc1) slab stores (else plain)
+constexpr int kBwdVarSlabFlat = 2, kBwdVarSlabWT = 4;
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
@@ -446,56 +449,64 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       const float* t0 = reinterpret_cast<const float*>(stage_b);
       constexpr int kSw = CT > 0 ? 64 / CT : 1;
       const bool full = CT > 0 && Sv == kSw && Sw == kSw;
-      // the wave's slab elements as one flat list over its degrees (ascending): element e
-      // -> global index g; eight per lane per pass with all their LDS loads issued first
-      int tot = 0;
-      each_degree([&](int l) { tot += (2 * l + 1) * C; });
-      auto gidx = [&](int e) {
-        int off = 0, g = 0;
-        each_degree([&](int l) {
-          const int cnt = (2 * l + 1) * C;
-          if (e >= off && e < off + cnt) g = l * l * C + (e - off);
-          off += cnt;
-        });
-        return g;
-      };
-      // write-through stores (sc1): the slabs leave the XCD's L2 while the kernel runs
-      // instead of as dirty lines written back at its end, ahead of the reduce kernel
+      // write-through (sc1, kBwdVarSlabWT) or plain slab stores
       const int64_t slab_floats = (int64_t)gridDim.x * (a.slab_chunked ? slab_chunks(MC) * kSlabChunk : MC);
       const __amdgpu_buffer_rsrc_t wrs =
           __builtin_amdgcn_make_buffer_rsrc(a.ws_F, 0, (int)(slab_floats * 4), kRawBufferFlags);
       const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
+      const bool wt = (a.variant & kBwdVarSlabWT) != 0;
       auto put = [&](int g, float sum) {
         const int64_t idx = a.slab_chunked ? (g / kSlabChunk) * cstride + (int64_t)blockIdx.x * kSlabChunk + g % kSlabChunk
                                            : (int64_t)blockIdx.x * MC + g;
-        tile_store_elem<16>(wrs, (int)(idx * 4), sum);
+        if (wt) tile_store_elem<16>(wrs, (int)(idx * 4), sum);
+        else a.ws_F[idx] = sum;
       };
-      if (full) {
-        constexpr int kU = 8;
-        for (int e0 = lane; e0 < tot; e0 += kU * 64) {
-          float v[kU][kSw];
-          int gg[kU];
+      // a range [g0, g0 + cnt) of slab elements, kU per lane per pass with all their LDS
+      // loads issued before any sum or store; idx maps a range position to the element
+      auto sum_range = [&](int cnt, auto&& idx) {
+        if (full) {
+          constexpr int kU = 4;
+          for (int e0 = lane; e0 < cnt; e0 += kU * 64) {
+            float v[kU][kSw];
+            int gg[kU];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) {
-            gg[u] = gidx(min(e0 + 64 * u, tot - 1));  // clamped: in-range reads
+            for (int u = 0; u < kU; ++u) {
+              gg[u] = idx(min(e0 + 64 * u, cnt - 1));  // clamped: in-range reads
 #pragma unroll
-            for (int jj = 0; jj < kSw; ++jj) v[u][jj] = t0[jj * MC + gg[u]];
+              for (int jj = 0; jj < kSw; ++jj) v[u][jj] = t0[jj * MC + gg[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+              float sum = v[u][0];
+#pragma unroll
+              for (int jj = 1; jj < kSw; ++jj) sum += v[u][jj];
+              if (e0 + 64 * u < cnt) put(gg[u], sum);
+            }
           }
-#pragma unroll
-          for (int u = 0; u < kU; ++u) {
-            float sum = v[u][0];
-#pragma unroll
-            for (int jj = 1; jj < kSw; ++jj) sum += v[u][jj];
-            if (e0 + 64 * u < tot) put(gg[u], sum);
+        } else {
+          for (int e = lane; e < cnt; e += 64) {
+            const int g = idx(e);
+            float sum = t0[g];
+            for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
+            put(g, sum);
           }
         }
+      };
+      if (a.variant & kBwdVarSlabFlat) {
+        // the wave's elements as one flat list over its degrees (ascending)
+        int tot = 0;
+        each_degree([&](int l) { tot += (2 * l + 1) * C; });
+        sum_range(tot, [&](int e) {
+          int off = 0, g = 0;
+          each_degree([&](int l) {
+            const int cnt = (2 * l + 1) * C;
+            if (e >= off && e < off + cnt) g = l * l * C + (e - off);
+            off += cnt;
+          });
+          return g;
+        });
       } else {
-        for (int e = lane; e < tot; e += 64) {
-          const int g = gidx(e);
-          float sum = t0[g];
-          for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + g];
-          put(g, sum);
-        }
+        each_degree([&](int l) { sum_range((2 * l + 1) * C, [&](int e) { return l * l * C + e; }); });
       }
     }
     phase_stamp(a.stamps, wave, 3);
