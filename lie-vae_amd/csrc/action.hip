@@ -147,6 +147,53 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce3_kernel(const float* w
   }
 }
 
+// Chunk-major slabs, fewer barriers: as action_bwd_reduce3_kernel, but the 16 slab streams
+// of a wave are combined by cross-lane shuffles (xor 4, 8, 16, 32: stream pairs, no
+// barrier), then the 16 waves' partials by one barrier and a 16-term sum in wave order.
+// Deterministic (a fixed order, different from reduce3's halving tree).
+__global__ __launch_bounds__(1024) void action_bwd_reduce4_kernel(const float* ws_F, float* gF, int64_t MC,
+                                                                  int nslab) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ f4 part[16][4];
+  const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
+  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)blockIdx.x * nslab * kSlabChunk) + q;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  int b = bs;
+  for (; b + 3 * 256 < nslab; b += 4 * 256) {
+    f4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = base[(int64_t)(b + u * 256) * 4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u];
+  }
+  {
+    f4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) v[u] = b + u * 256 < nslab ? base[(int64_t)(b + u * 256) * 4] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (b + u * 256 < nslab) acc += v[u];
+  }
+#pragma unroll
+  for (int m = 4; m <= 32; m <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+  }
+  const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  if (lane < 4) part[w][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    f4 r = part[0][q];
+#pragma unroll
+    for (int ww = 1; ww < 16; ++ww) r += part[ww][q];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = (int64_t)blockIdx.x * kSlabChunk + 4 * q + k;
+      if (e < MC) gF[e] = r[k];
+    }
+  }
+}
+
 namespace {
 
 template <int... Ls>
@@ -616,7 +663,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // dF slab reduce: LV_BWD_REDUCE (A/B) 3 = chunk-major slabs + action_bwd_reduce3_kernel,
   // 16 / 8 / 4 = row slabs + action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
   static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
-  p.a.slab_chunked = b.fmode != kBwdFSample && kEnvReduce == 3;
+  p.a.slab_chunked = b.fmode != kBwdFSample && (kEnvReduce == 3 || kEnvReduce == 5);
   static const int kEnvVariant = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
   p.a.variant = kEnvVariant;
   p.a.stamps = ab_stamps();
@@ -634,6 +681,11 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // 4,096, 187 vs 191 at 65,536, 9.9 vs 9.8 at 512 against reduce2<16>, the round-3
   // default; an in-kernel reduction by the tile kernel's last blocks -- completion counter,
   // device-scope release fences -- ran 75 us per call at 4,096 and was dropped)
+  if (p.a.slab_chunked && kEnvReduce == 5) {
+    hipLaunchKernelGGL(action_bwd_reduce4_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
+                       (const float*)workspace, gF, MC, b.gx);
+    LV_RETURN_LAUNCH("action_bwd_reduce4_kernel");
+  }
   if (p.a.slab_chunked) {
     hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
                        (const float*)workspace, gF, MC, b.gx, p.a.stamps);
