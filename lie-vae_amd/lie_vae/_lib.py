@@ -154,6 +154,23 @@ def plan(kind, *args):
     return d
 
 
+TORCH_OPS_PATH = os.environ.get("LIEVAE_TORCH_OPS_LIB", os.path.join(_HERE, "liblievae_torch.so"))
+_torch_ops = None
+
+
+def load_torch_ops():
+    """Register the C++ operators of liblievae_torch.so (csrc/torch_ops.cpp) with torch
+    once; False when that library is not built (the Python autograd path is used then)."""
+    global _torch_ops
+    if _torch_ops is None:
+        _torch_ops = False
+        if os.path.exists(TORCH_OPS_PATH):
+            load()  # the kernels' library first (the operators link against it)
+            torch.ops.load_library(TORCH_OPS_PATH)
+            _torch_ops = True
+    return _torch_ops
+
+
 def stream():
     """The caller's current HIP stream (raw handle, as an int)."""
     return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device())

@@ -331,10 +331,16 @@ class _FusedExpAction(torch.autograd.Function):
         return gmu, gv, gspec, None, None, None
 
 
+_TORCH_OPS = _lib.load_torch_ops()  # liblievae_torch.so: the op as a C++ autograd function
+
+
 def fused_exp_action(mu, v, spectrum, L, transpose=False, out_dtype=F32):
     """(mu (n,3,3) or None, v (n,3), spectrum (M,C) or a stride-0 expand of it) ->
     (n, M, C).  The fused kernel takes a shared spectrum only (ActionNet's item_rep);
-    a per-sample spectrum goes through group_action."""
+    a per-sample spectrum goes through group_action.  Runs as the C++ operator
+    torch.ops.lievae.fused_exp_action (csrc/torch_ops.cpp: forward, backward and autograd
+    bookkeeping without Python frames) when liblievae_torch.so is built, else through the
+    Python autograd.Function below -- the same kernels either way."""
     assert v.dim() == 2 and v.shape[1] == 3, f"v must be (n,3), got {tuple(v.shape)}"
     n = v.shape[0]
     if mu is not None:
@@ -344,6 +350,9 @@ def fused_exp_action(mu, v, spectrum, L, transpose=False, out_dtype=F32):
         raise ValueError("fused_exp_action takes a shared (M,C) spectrum; use group_action "
                          "for a per-sample (n,M,C) spectrum")
     _lib.require_device(v, spectrum, mu)
+    if _TORCH_OPS:
+        return torch.ops.lievae.fused_exp_action(mu, v, spectrum, L, bool(transpose),
+                                                 out_dtype == torch.bfloat16)
     return _FusedExpAction.apply(mu, v, _f32c(spectrum), L, transpose, out_dtype)
 
 
