@@ -6,7 +6,8 @@
 # trace (with find enabled every new process searches again).  Per variant: the timing
 # JSON with and without find, a rocprofv3 kernel-trace (--stats) and one PMC pass for
 # MFMA utilisation per kernel.
-#   bash tools/gpu_train_prof.sh [variant ...]   variants: f32 bf16 f32_nogemm bf16_nogemm
+#   bash tools/gpu_train_prof.sh [variant ...]   variants: f32 bf16 f32_nogemm bf16_nogemm bf16_transposed
+#   bf16_norelu bf16_miodgrad bf16_foreach
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/train_prof
@@ -27,18 +28,10 @@ for v in $VARIANTS; do
     bf16) A="--amp bf16 --channels-last" ;;
     f32_nogemm) A="--conv-gemm off" ;;
     bf16_nogemm) A="--amp bf16 --channels-last --conv-gemm off" ;;
-    bf16_nbn) A="--amp bf16 --channels-last --bn native" ;;
-    bf16_gemv) A="--amp bf16 --channels-last --bias-grad gemv" ;;
-    bf16_both) A="--amp bf16 --channels-last --bn native --bias-grad gemv" ;;
-    f32_nbn) A="--bn native" ;;
-    bf16_phase) A="--amp bf16 --channels-last --bn native --deconv phase" ;;
-    bf16_mfma) A="--amp bf16 --channels-last --bn native --deconv mfma" ;;
-    bf16_norelu) A="--amp bf16 --channels-last --bn native --deconv mfma --fused-relu off" ;;
-    bf16_miodgrad) A="--amp bf16 --channels-last --bn native --deconv mfma --conv-dgrad miopen" ;;
-    bf16_foreach) A="--amp bf16 --channels-last --bn native --deconv mfma --adam foreach" ;;
-    bf16_nbn2) A="--amp bf16 --channels-last --bn native" ;;
-    f32_phase) A="--bn native --deconv phase" ;;
-    f32_both) A="--bn native --bias-grad gemv" ;;
+    bf16_transposed) A="--amp bf16 --channels-last --deconv transposed" ;;
+    bf16_norelu) A="--amp bf16 --channels-last --fused-relu off" ;;
+    bf16_miodgrad) A="--amp bf16 --channels-last --conv-dgrad miopen" ;;
+    bf16_foreach) A="--amp bf16 --channels-last --adam foreach" ;;
     *) echo "unknown variant $v"; exit 2 ;;
   esac
   step warm_$v 600 python bench_train.py --steps 3 --warmup 2 $A
