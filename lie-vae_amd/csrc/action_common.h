@@ -88,52 +88,6 @@ __device__ __forceinline__ void quat_to_zyz_trig(const float q[4], float c1[3], 
 // (lie_tools.py:126-156).  cos(beta) = 1 - (1 - cb) is formed in "one-minus" form so that
 // sin(beta) = sqrt((1-cb)(1+cb)) keeps full relative accuracy near beta = 0 / pi, where the
 // reference's fp32 acos(cb) loses it (the clamp to +-(1 - 1e-6) is mirrored exactly).
-__device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], float s1[3],
-                                                float qr[4]) {
-  const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-  const float inv = rsqrtf(vv);  // NaN downstream at v = 0, as the reference
-  const float th = vv * inv;
-  float sh, ch;
-  sincosf(0.5f * th, &sh, &ch);
-  const float m = -sh * inv;
-  const float qt[4] = {v[0] * m, v[1] * m, v[2] * m, ch};
-  int k = 0;
-  float best = fabsf(qt[0]);
-#pragma unroll
-  for (int i = 1; i < 4; ++i)
-    if (fabsf(qt[i]) > best) { best = fabsf(qt[i]); k = i; }
-  const float qk = k == 0 ? qt[0] : (k == 1 ? qt[1] : (k == 2 ? qt[2] : qt[3]));
-  constexpr float eps = 2.5e-7f;
-  const float qk2 = qk * qk;
-  // d = sqrt(qk^2 + eps), best / d as reciprocal-square-root products (<= 2 ulp)
-  const float rd = rsqrtf(qk2 + eps);
-  const float d = (qk2 + eps) * rd;
-  const float sc = copysignf(best * rd, qk);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
-  const float oms = eps * (1.f - 2.f * qk2 - eps) / (qk2 + eps);  // 1 - |q_ref|^2
-  float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
-  float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
-  constexpr float kDelta = 1.f - kEazyzHi;                          // exact in fp32
-  if (omc < kDelta) { omc = kDelta; opc = 2.f - kDelta; }
-  else if (opc < kDelta) { opc = kDelta; omc = 2.f - kDelta; }
-  c1[1] = omc <= opc ? 1.f - omc : opc - 1.f;
-  s1[1] = __builtin_amdgcn_sqrtf(omc * opc);  // v_sqrt_f32 (1 ulp)
-  auto dir = [](float y, float x, float& c, float& s) {
-    const float r2 = x * x + y * y;
-    if (r2 == 0.f) {  // atan2(+-0, +-0) in {0, +-pi}
-      c = signbit(x) ? -1.f : 1.f;
-      s = 0.f;
-    } else {
-      const float r = rsqrtf(r2);
-      c = x * r;
-      s = y * r;
-    }
-  };
-  dir(qr[1] * qr[2] - qr[0] * qr[3], qr[0] * qr[2] + qr[1] * qr[3], c1[0], s1[0]);
-  dir(qr[0] * qr[3] + qr[1] * qr[2], qr[1] * qr[3] - qr[0] * qr[2], c1[2], s1[2]);
-}
-
 // sin and cos of x as straight-line code: Cody-Waite reduction by pi/2 (three-part fp32
 // constant, FMA) into [-pi/4, pi/4], minimax polynomials (the Cephes sinf / cosf
 // coefficients) and the quadrant by k & 3; <= 1.6 ulp for |x| <= 1e5 (checked against fp64
@@ -160,12 +114,14 @@ __device__ __forceinline__ void lv_sincos(float x, float& s, float& c) {
   if (__builtin_expect(!(fabsf(x) <= 1.0e5f), 0)) sincosf(x, &s, &c);
 }
 
-// One slot of exp_to_zyz_trig (angle index ai: 0 = alpha, 1 = beta, 2 = gamma) as
-// straight-line code (selects, no divergent branches): each prologue thread of the tile
-// kernel fills one slot's multiples, so it computes that slot's (cos, sin) only (and the
-// quaternion, for ang_out).  Same formulas as exp_to_zyz_trig; lv_sincos for the half
-// angle and rsqrt products for the divisions (<= 2 ulp).
-__device__ __forceinline__ void exp_to_zyz_slot(const float v[3], int ai, float& c, float& s, float qr[4]) {
+// The quaternion part of exp_to_zyz_trig: q_ref of z = exp(v) (see exp_to_zyz_trig), and the
+// quantities the angle formulas reuse.
+struct ExpQuat {
+  float qr[4];
+  float qk2, rd;  // the largest component squared, rsqrt(qk2 + eps)
+};
+__device__ __forceinline__ ExpQuat exp_quat(const float v[3]) {
+  ExpQuat e;
   const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
   const float inv = rsqrtf(vv);  // NaN downstream at v = 0, as the reference
   const float th = vv * inv;
@@ -180,31 +136,74 @@ __device__ __forceinline__ void exp_to_zyz_slot(const float v[3], int ai, float&
     if (fabsf(qt[i]) > best) { best = fabsf(qt[i]); k = i; }
   const float qk = k == 0 ? qt[0] : (k == 1 ? qt[1] : (k == 2 ? qt[2] : qt[3]));
   constexpr float eps = 2.5e-7f;
-  const float qk2 = qk * qk;
-  const float rd = rsqrtf(qk2 + eps);
-  const float d = (qk2 + eps) * rd;
-  const float sc = copysignf(best * rd, qk);
+  e.qk2 = qk * qk;
+  // d = sqrt(qk^2 + eps), best / d as reciprocal-square-root products (<= 2 ulp)
+  e.rd = rsqrtf(e.qk2 + eps);
+  const float d = (e.qk2 + eps) * e.rd;
+  const float sc = copysignf(best * e.rd, qk);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) qr[i] = (i == k) ? d : qt[i] * sc;
-  // beta: cos from the "one-minus" forms, clamp to +-(1 - 1e-6) mirrored
-  const float oms = eps * (1.f - 2.f * qk2 - eps) * (rd * rd);       // 1 - |q_ref|^2
-  float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);        // 1 - cos(beta)
-  float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);        // 1 + cos(beta)
+  for (int i = 0; i < 4; ++i) e.qr[i] = (i == k) ? d : qt[i] * sc;
+  return e;
+}
+// (cos, sin) of beta: cos from the "one-minus" forms, the clamp to +-(1 - 1e-6) mirrored
+__device__ __forceinline__ void exp_beta(const ExpQuat& e, float& c, float& s) {
+  constexpr float eps = 2.5e-7f;
+  const float* qr = e.qr;
+  const float oms = eps * (1.f - 2.f * e.qk2 - eps) * (e.rd * e.rd);  // 1 - |q_ref|^2
+  float omc = fmaf(2.f, qr[0] * qr[0] + qr[1] * qr[1], oms);          // 1 - cos(beta)
+  float opc = fmaf(2.f, qr[2] * qr[2] + qr[3] * qr[3], oms);          // 1 + cos(beta)
   constexpr float kDelta = 1.f - kEazyzHi;
   const bool clo = omc < kDelta, chi = !clo && opc < kDelta;
   omc = clo ? kDelta : (chi ? 2.f - kDelta : omc);
   opc = clo ? 2.f - kDelta : (chi ? kDelta : opc);
-  const float cb = omc <= opc ? 1.f - omc : opc - 1.f;
-  const float sb = __builtin_amdgcn_sqrtf(omc * opc);
-  // alpha / gamma: the direction of (x, y), atan2(+-0, +-0) in {0, +-pi} mirrored
+  c = omc <= opc ? 1.f - omc : opc - 1.f;
+  s = __builtin_amdgcn_sqrtf(omc * opc);  // v_sqrt_f32 (1 ulp)
+}
+// (cos, sin) of alpha (ai = 0) or gamma (ai = 2): the direction of (x, y), atan2(+-0, +-0)
+// in {0, +-pi} mirrored
+__device__ __forceinline__ void exp_dir(const ExpQuat& e, int ai, float& c, float& s) {
+  const float* qr = e.qr;
   const float y = ai == 0 ? qr[1] * qr[2] - qr[0] * qr[3] : qr[0] * qr[3] + qr[1] * qr[2];
   const float x = ai == 0 ? qr[0] * qr[2] + qr[1] * qr[3] : qr[1] * qr[3] - qr[0] * qr[2];
   const float r2 = x * x + y * y;
   const float rr = rsqrtf(r2);
-  const float cd = r2 == 0.f ? (signbit(x) ? -1.f : 1.f) : x * rr;
-  const float sd = r2 == 0.f ? 0.f : y * rr;
+  c = r2 == 0.f ? (signbit(x) ? -1.f : 1.f) : x * rr;
+  s = r2 == 0.f ? 0.f : y * rr;
+}
+
+// (cos, sin) of the three ZYZ angles of z = exp(v) straight from the axis-angle form, at
+// better than fp32-reference accuracy.  The reference's q = group_matrix_to_quaternions(
+// rodrigues(v)) is, in exact arithmetic, the unit quaternion q* = (-u sin(t/2), cos(t/2))
+// of R(v) (its matrix is the transpose of the active one) with the trace method's epsilon
+// applied to the largest component k: q_k -> d = sqrt(q_k^2 + 2.5e-7), q_j -> sign(q_k)
+// q_j |q_k| / d (lie_tools.py:126-156).  cos(beta) = 1 - (1 - cb) is formed in "one-minus"
+// form so that sin(beta) = sqrt((1-cb)(1+cb)) keeps full relative accuracy near beta = 0 /
+// pi, where the reference's fp32 acos(cb) loses it (the clamp to +-(1 - 1e-6) is mirrored
+// exactly).  Every fused kernel evaluates these same expressions (bitwise equal across the
+// tile and non-tile kernels).
+__device__ __forceinline__ void exp_to_zyz_trig(const float v[3], float c1[3], float s1[3],
+                                                float qr[4]) {
+  const ExpQuat e = exp_quat(v);
+  exp_dir(e, 0, c1[0], s1[0]);
+  exp_beta(e, c1[1], s1[1]);
+  exp_dir(e, 2, c1[2], s1[2]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qr[i] = e.qr[i];
+}
+
+// One slot (angle index ai: 0 = alpha, 1 = beta, 2 = gamma) of exp_to_zyz_trig, straight-
+// line (selects, no divergent branches): each prologue thread of the tile kernel fills one
+// slot's multiples, so it computes that slot's (cos, sin) only (and the quaternion, for
+// ang_out).  Bitwise the values exp_to_zyz_trig returns for that slot.
+__device__ __forceinline__ void exp_to_zyz_slot(const float v[3], int ai, float& c, float& s, float qr[4]) {
+  const ExpQuat e = exp_quat(v);
+  float cb, sb, cd, sd;
+  exp_beta(e, cb, sb);
+  exp_dir(e, ai, cd, sd);
   c = ai == 1 ? cb : cd;
   s = ai == 1 ? sb : sd;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qr[i] = e.qr[i];
 }
 
 // General mean (z = mu @ exp(v)): the reference's op sequence (rodrigues, matmul, trace
