@@ -59,6 +59,8 @@ class BucketedAllReduce:
                 off += p.numel()
             self.state.append({"buf": buf, "left": len(plist), "handle": None})
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        for p in self.params:  # gradients that bypass AccumulateGrad (nets._CachedCast)
+            p._lv_grad_sink = self._on_grad
 
     def _on_grad(self, p):
         st = self.state[self.owner[p]]
