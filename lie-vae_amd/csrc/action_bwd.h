@@ -209,7 +209,6 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   constexpr bool SHAREDF = FM != kBwdFSample;
   constexpr bool GSLAB = FM == kBwdFSharedGlobal;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int kRow = TrigLds<LT>::kRow;
   const int C = CT > 0 ? CT : a.C;
   const int Sw = a.Sw;
