@@ -487,6 +487,66 @@ def test_fused_exp_action_bwd_matches_modular_bitwise(gpu_device):
                 assert torch.equal(gmu1, gmu2), what
 
 
+def test_fused_torch_operator_matches_python_function_bitwise(gpu_device):
+    """torch.ops.lievae.fused_exp_action (csrc/torch_ops.cpp, the C++ autograd function the
+    product calls) against the Python autograd.Function over the same C ABI: outputs and
+    gradients bit for bit, with and without a mean, transposed, bf16 output, fp64 inputs
+    (gradients come back in the inputs' dtypes), and under hipGraph capture."""
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    assert ops._TORCH_OPS, "liblievae_torch.so not loaded: the product's operator is missing"
+    torch.manual_seed(11)
+    for L, C, n, transpose, odt, idt, with_mu in [
+            (10, 10, 4096, False, torch.float32, torch.float32, False),
+            (10, 10, 1001, True, torch.float32, torch.float32, True),
+            (20, 10, 777, False, torch.bfloat16, torch.float32, False),
+            (6, 7, 300, False, torch.float32, torch.float64, True)]:
+        M = (L + 1) ** 2
+        v0 = torch.randn(n, 3, device=gpu_device, dtype=idt)
+        F0 = torch.randn(M, C, device=gpu_device, dtype=idt)
+        mu0 = lt.random_group_matrices(n, device=gpu_device).to(idt).contiguous() if with_mu else None
+        gout = torch.randn(n, M, C, device=gpu_device, dtype=odt)
+        res = []
+        for use_op in (True, False):
+            v, F = v0.clone().requires_grad_(True), F0.clone().requires_grad_(True)
+            mu = mu0.clone().requires_grad_(True) if with_mu else None
+            if use_op:
+                out = torch.ops.lievae.fused_exp_action(mu, v, F, L, transpose, odt == torch.bfloat16)
+            else:
+                out = ops._FusedExpAction.apply(mu, v, ops._f32c(F), L, transpose, odt)
+            out.backward(gout)
+            res.append((out, v.grad, F.grad, mu.grad if with_mu else None))
+        what = (L, C, n, transpose, odt, idt, with_mu)
+        (o1, gv1, gF1, gm1), (o2, gv2, gF2, gm2) = res
+        assert o1.dtype == odt and gv1.dtype == idt and gF1.dtype == idt, what
+        assert torch.equal(o1, o2), what
+        assert torch.equal(gv1, gv2.to(idt)), what
+        assert torch.equal(gF1, gF2.to(idt)), what
+        if with_mu:
+            assert gm1.dtype == idt and torch.equal(gm1, gm2.to(idt)), what
+    # the operator under graph capture (fresh workspace from the capture pool)
+    n, L, C = 4096, 10, 10
+    v = torch.randn(n, 3, device=gpu_device, requires_grad=True)
+    F = torch.randn((L + 1) ** 2, C, device=gpu_device, requires_grad=True)
+    gout = torch.randn(n, (L + 1) ** 2, C, device=gpu_device)
+    side = torch.cuda.Stream(gpu_device)
+    side.wait_stream(torch.cuda.current_stream(gpu_device))
+    with torch.cuda.stream(side):
+        out = torch.ops.lievae.fused_exp_action(None, v, F, L, False, False)
+        out.backward(gout)
+    torch.cuda.current_stream(gpu_device).wait_stream(side)
+    ref = (out.detach().clone(), v.grad.clone(), F.grad.clone())
+    v.grad = None
+    F.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out_g = torch.ops.lievae.fused_exp_action(None, v, F, L, False, False)
+        out_g.backward(gout)
+    g.replay()
+    torch.cuda.synchronize(gpu_device)
+    assert torch.equal(out_g, ref[0]) and torch.equal(v.grad, ref[1]) and torch.equal(F.grad, ref[2])
+
+
 def test_fused_vs_oracle_config2(gpu_device):
     """Config 2 exactly: B=4096, l=10, C=10, v ~ N(0,1), shared F (no mu)."""
     import lie_vae._ops as ops
