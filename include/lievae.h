@@ -252,6 +252,10 @@ int lv_bn_lrelu_fwd_bf16(const void* x, const float* gamma, const float* beta, f
 int lv_bn_lrelu_bwd_bf16(const void* g, const void* x, const float* gamma, const float* beta,
                          const float* save_mean, const float* save_invstd, float slope, void* gx,
                          float* ggamma, float* gbeta, float* ws, int64_t P, int C, void* stream);
+/* acc[i] += (float)g[i], i < n: a bf16 parameter gradient (the autocast copy's) added in
+ * place into its fp32 master gradient, one pass (replaces the cast + AccumulateGrad add pair
+ * of torch.autocast's weight casts in the bf16 training step; deterministic). */
+int lv_accumulate_bf16_f32(const void* g, float* acc, int64_t n, void* stream);
 /* Fused ReLU around the decoder layers (DeconvNet's nn.ReLU, nets.py:62-72), flags:
  *   LV_DECONV_RELU_OUT  y = max(conv_transpose(x) + b, 0) (the ReLU after the layer);
  *   LV_DECONV_MASK_GX   (backward, small-Cout layer) gx masked by x > 0 only: x is already a

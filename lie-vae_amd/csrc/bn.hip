@@ -302,6 +302,33 @@ bool bn_geom(int64_t P, int C, BnGeom* g) {
   return true;
 }
 
+// acc[i] += g[i] (bf16 -> fp32): a parameter's bf16 gradient (the autocast copy's) added
+// into its fp32 master gradient in one pass, 10 bytes per element.  VEC = 4: 8-byte bf16
+// and 16-byte fp32 accesses (both pointers aligned to them); 1 otherwise.
+template <int VEC>
+__global__ __launch_bounds__(256) void accumulate_bf16_f32_kernel(const __hip_bfloat16* __restrict__ g,
+                                                                  float* __restrict__ acc, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nv = n / VEC;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    if constexpr (VEC == 4) {
+      const uint2 gv = reinterpret_cast<const uint2*>(g)[i];
+      float4 a = reinterpret_cast<float4*>(acc)[i];
+      a.x += __uint_as_float(gv.x << 16);
+      a.y += __uint_as_float(gv.x & 0xffff0000u);
+      a.z += __uint_as_float(gv.y << 16);
+      a.w += __uint_as_float(gv.y & 0xffff0000u);
+      reinterpret_cast<float4*>(acc)[i] = a;
+    } else {
+      acc[i] += __bfloat162float(g[i]);
+    }
+  }
+  if constexpr (VEC > 1) {  // the last n % VEC elements
+    const int64_t t = nv * VEC + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && t < n) acc[t] += __bfloat162float(g[t]);
+  }
+}
+
 int apply_blocks(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, (nvec + kBnThreads - 1) / kBnThreads)); }
 
 }  // namespace
@@ -310,6 +337,24 @@ int apply_blocks(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64
 using namespace lv;
 
 extern "C" {
+
+int lv_accumulate_bf16_f32(const void* g, float* acc, int64_t n, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(n >= 0, "n < 0");
+  if (n == 0) return LV_OK;
+  LV_CHECK_ARG(g && acc, "null pointer");
+  const bool vec = (reinterpret_cast<uintptr_t>(g) & 7) == 0 && (reinterpret_cast<uintptr_t>(acc) & 15) == 0;
+  const int64_t units = vec ? n / 4 : n;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (units + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (vec)
+    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<4>, dim3(blocks), dim3(256), 0, st,
+                       (const __hip_bfloat16*)g, acc, n);
+  else
+    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<1>, dim3(blocks), dim3(256), 0, st,
+                       (const __hip_bfloat16*)g, acc, n);
+  LV_RETURN_LAUNCH("accumulate_bf16_f32_kernel");
+}
 
 int lv_bn_supported(int64_t P, int C) {
   BnGeom g;

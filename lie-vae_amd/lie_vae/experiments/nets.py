@@ -38,9 +38,11 @@ def _cl(t):
 class _CachedCast(torch.autograd.Function):
     """Backward: the cast's (gradient to fp32) -- or, when the parameter's .grad is a
     gradient-bucket view of DPTrainer (``p._lv_grad_sink`` set by BucketedAllReduce), the
-    bf16 gradient added into .grad by one mixed-dtype in-place add and the bucket's
-    post-accumulate hook called directly: one kernel per parameter instead of a cast and
-    AccumulateGrad's add (22 + 22 tiny kernels per config-3 step)."""
+    bf16 gradient added into .grad in place by the library's one-pass kernel
+    (lv_accumulate_bf16_f32; torch's mixed-dtype add_ runs a non-vectorised kernel, ~50 us
+    per conv weight) and the bucket's post-accumulate hook called directly: one kernel per
+    parameter instead of a cast and AccumulateGrad's add (22 + 22 tiny kernels per config-3
+    step)."""
 
     @staticmethod
     def forward(ctx, p, pb):
@@ -52,8 +54,16 @@ class _CachedCast(torch.autograd.Function):
     def backward(ctx, g):
         p = ctx.p
         sink = getattr(p, "_lv_grad_sink", None)
-        if sink is not None and p.grad is not None and not torch.is_grad_enabled():
-            p.grad.add_(g)
+        gr = p.grad
+        if sink is not None and gr is not None and not torch.is_grad_enabled():
+            if (g.dtype == torch.bfloat16 and gr.dtype == torch.float32 and g.shape == gr.shape
+                    and g.stride() == gr.stride()
+                    and (gr.is_contiguous() or (gr.dim() == 4 and gr.is_contiguous(memory_format=torch.channels_last)))):
+                from .. import _lib
+                _lib.call("lv_accumulate_bf16_f32", g.data_ptr(), gr.data_ptr(), gr.numel(),
+                          _lib.stream_of(gr.device))
+            else:
+                gr.add_(g)
             sink(p)
             return None, None
         return g.to(ctx.dt), None

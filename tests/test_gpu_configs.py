@@ -915,3 +915,20 @@ def test_fused_bn_leaky_relu_matches_float64(gpu_device, N, C, H, W):
         rms = ref.square().mean().sqrt()
         bad = (gd - ref).abs() > loose * (rel * ref.abs() + absr * rms)
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max {(gd - ref).abs().max():.3e}"
+
+
+def test_accumulate_bf16_into_f32_bitwise(gpu_device):
+    """lv_accumulate_bf16_f32 (the bf16 training step's master-gradient accumulation,
+    nets.py _CachedCast) against torch's acc + g.float(): bit for bit, on aligned (vector
+    path) and misaligned (scalar path) pointers, sizes with a ragged tail, and n = 0."""
+    from lie_vae._lib import call, stream
+    torch.manual_seed(3)
+    for n, off_g, off_a in [(0, 0, 0), (1, 0, 0), (7, 0, 0), (4096 * 9 + 3, 0, 0), (1000, 1, 0),
+                            (1000, 0, 1), (2_000_003, 0, 0)]:
+        gb = torch.randn(n + off_g, device=gpu_device).to(torch.bfloat16)
+        ab = torch.randn(n + off_a, device=gpu_device)
+        g, a = gb[off_g:], ab[off_a:]
+        ref = a + g.float()
+        call("lv_accumulate_bf16_f32", g.data_ptr(), a.data_ptr(), n, stream())
+        torch.cuda.synchronize(gpu_device)
+        assert torch.equal(a, ref), (n, off_g, off_a)
