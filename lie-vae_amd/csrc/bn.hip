@@ -303,30 +303,44 @@ bool bn_geom(int64_t P, int C, BnGeom* g) {
 }
 
 // acc[i] += g[i] (bf16 -> fp32): a parameter's bf16 gradient (the autocast copy's) added
-// into its fp32 master gradient in one pass, 10 bytes per element.  VEC = 4: 8-byte bf16
-// and 16-byte fp32 accesses (both pointers aligned to them); 1 otherwise.
-template <int VEC>
+// into its fp32 master gradient in one pass, 10 bytes per element.  The first `head` (< 4)
+// elements are peeled so that acc + head is 16-byte aligned (gradient-bucket views start
+// anywhere); the body moves 4 elements per lane: one 16-byte fp32 access and, by g's
+// alignment there, one 8-byte (GA = 8), two 4-byte (GA = 4) or four 2-byte (GA = 2) reads.
+__device__ __forceinline__ float bf16_bits_to_float(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
+
+template <int GA>
 __global__ __launch_bounds__(256) void accumulate_bf16_f32_kernel(const __hip_bfloat16* __restrict__ g,
-                                                                  float* __restrict__ acc, int64_t n) {
+                                                                  float* __restrict__ acc, int64_t n, int head) {
+  const unsigned short* gb = reinterpret_cast<const unsigned short*>(g);
+  const int tid0 = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (blockIdx.x == 0 && (int)threadIdx.x < head && threadIdx.x < n)
+    acc[threadIdx.x] += bf16_bits_to_float(gb[threadIdx.x]);
+  const int64_t nv = (n - head) / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t nv = n / VEC;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
-    if constexpr (VEC == 4) {
-      const uint2 gv = reinterpret_cast<const uint2*>(g)[i];
-      float4 a = reinterpret_cast<float4*>(acc)[i];
-      a.x += __uint_as_float(gv.x << 16);
-      a.y += __uint_as_float(gv.x & 0xffff0000u);
-      a.z += __uint_as_float(gv.y << 16);
-      a.w += __uint_as_float(gv.y & 0xffff0000u);
-      reinterpret_cast<float4*>(acc)[i] = a;
+  float4* a4 = reinterpret_cast<float4*>(acc + head);
+  const unsigned short* gh = gb + head;
+  for (int64_t i = tid0; i < nv; i += stride) {
+    float x0, x1, x2, x3;
+    if constexpr (GA == 8) {
+      const uint2 v = reinterpret_cast<const uint2*>(gh)[i];
+      x0 = __uint_as_float(v.x << 16), x1 = __uint_as_float(v.x & 0xffff0000u);
+      x2 = __uint_as_float(v.y << 16), x3 = __uint_as_float(v.y & 0xffff0000u);
+    } else if constexpr (GA == 4) {
+      const unsigned v0 = reinterpret_cast<const unsigned*>(gh)[2 * i];
+      const unsigned v1 = reinterpret_cast<const unsigned*>(gh)[2 * i + 1];
+      x0 = __uint_as_float(v0 << 16), x1 = __uint_as_float(v0 & 0xffff0000u);
+      x2 = __uint_as_float(v1 << 16), x3 = __uint_as_float(v1 & 0xffff0000u);
     } else {
-      acc[i] += __bfloat162float(g[i]);
+      x0 = bf16_bits_to_float(gh[4 * i]), x1 = bf16_bits_to_float(gh[4 * i + 1]);
+      x2 = bf16_bits_to_float(gh[4 * i + 2]), x3 = bf16_bits_to_float(gh[4 * i + 3]);
     }
+    float4 a = a4[i];
+    a.x += x0, a.y += x1, a.z += x2, a.w += x3;
+    a4[i] = a;
   }
-  if constexpr (VEC > 1) {  // the last n % VEC elements
-    const int64_t t = nv * VEC + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blockIdx.x == 0 && t < n) acc[t] += __bfloat162float(g[t]);
-  }
+  const int64_t t = head + nv * 4 + tid0;  // the last (n - head) % 4 elements
+  if (blockIdx.x == 0 && t < n) acc[t] += bf16_bits_to_float(gb[t]);
 }
 
 int apply_blocks(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, (nvec + kBnThreads - 1) / kBnThreads)); }
@@ -343,16 +357,20 @@ int lv_accumulate_bf16_f32(const void* g, float* acc, int64_t n, void* stream) {
   LV_CHECK_ARG(n >= 0, "n < 0");
   if (n == 0) return LV_OK;
   LV_CHECK_ARG(g && acc, "null pointer");
-  const bool vec = (reinterpret_cast<uintptr_t>(g) & 7) == 0 && (reinterpret_cast<uintptr_t>(acc) & 15) == 0;
-  const int64_t units = vec ? n / 4 : n;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (units + 255) / 256));
+  LV_CHECK_ARG((reinterpret_cast<uintptr_t>(g) & 1) == 0 && (reinterpret_cast<uintptr_t>(acc) & 3) == 0,
+               "misaligned element pointers");
+  const int head = (int)std::min<int64_t>(n, ((16 - (reinterpret_cast<uintptr_t>(acc) & 15)) & 15) / 4);
+  const uintptr_t gh = reinterpret_cast<uintptr_t>(g) + 2 * head;
+  const int64_t units = (n - head) / 4;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (units + 255) / 256));
   hipStream_t st = (hipStream_t)stream;
-  if (vec)
-    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<4>, dim3(blocks), dim3(256), 0, st,
-                       (const __hip_bfloat16*)g, acc, n);
+  const __hip_bfloat16* gp = (const __hip_bfloat16*)g;
+  if ((gh & 7) == 0)
+    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<8>, dim3(blocks), dim3(256), 0, st, gp, acc, n, head);
+  else if ((gh & 3) == 0)
+    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<4>, dim3(blocks), dim3(256), 0, st, gp, acc, n, head);
   else
-    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<1>, dim3(blocks), dim3(256), 0, st,
-                       (const __hip_bfloat16*)g, acc, n);
+    hipLaunchKernelGGL(accumulate_bf16_f32_kernel<2>, dim3(blocks), dim3(256), 0, st, gp, acc, n, head);
   LV_RETURN_LAUNCH("accumulate_bf16_f32_kernel");
 }
 

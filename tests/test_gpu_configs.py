@@ -919,12 +919,14 @@ def test_fused_bn_leaky_relu_matches_float64(gpu_device, N, C, H, W):
 
 def test_accumulate_bf16_into_f32_bitwise(gpu_device):
     """lv_accumulate_bf16_f32 (the bf16 training step's master-gradient accumulation,
-    nets.py _CachedCast) against torch's acc + g.float(): bit for bit, on aligned (vector
-    path) and misaligned (scalar path) pointers, sizes with a ragged tail, and n = 0."""
+    nets.py _CachedCast) against torch's acc + g.float(): bit for bit, for every alignment
+    of the two pointers (peeled head, 8 / 4 / 2-byte gradient reads), sizes with a ragged
+    tail, and n = 0."""
     from lie_vae._lib import call, stream
     torch.manual_seed(3)
-    for n, off_g, off_a in [(0, 0, 0), (1, 0, 0), (7, 0, 0), (4096 * 9 + 3, 0, 0), (1000, 1, 0),
-                            (1000, 0, 1), (2_000_003, 0, 0)]:
+    cases = [(0, 0, 0), (1, 0, 0), (2, 0, 3), (7, 0, 0), (4096 * 9 + 3, 0, 0), (2_000_003, 0, 0)]
+    cases += [(1001, og, oa) for og in range(4) for oa in range(4)]  # every alignment pair
+    for n, off_g, off_a in cases:
         gb = torch.randn(n + off_g, device=gpu_device).to(torch.bfloat16)
         ab = torch.randn(n + off_a, device=gpu_device)
         g, a = gb[off_g:], ab[off_a:]
