@@ -125,6 +125,35 @@ def test_empty_batches(gpu_device):
     assert out.shape == (0, 16, 4)
 
 
+def test_fused_operator_empty_and_single_sample(gpu_device):
+    """The product's operator (torch.ops.lievae.fused_exp_action) at n = 0 -- empty output,
+    a zero spectrum gradient -- and n = 1 (one partial sample group) against the modular
+    path, forward and backward."""
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    L, C = 10, 10
+    M = (L + 1) ** 2
+    F = torch.randn(M, C, device=gpu_device, requires_grad=True)
+    v = torch.zeros(0, 3, device=gpu_device, requires_grad=True)
+    out = ops.fused_exp_action(None, v, F, L)
+    assert out.shape == (0, M, C)
+    out.backward(torch.zeros(0, M, C, device=gpu_device))
+    assert F.grad is not None and torch.count_nonzero(F.grad) == 0 and v.grad.shape == (0, 3)
+    F.grad = None
+    torch.manual_seed(5)
+    v1 = torch.randn(1, 3, device=gpu_device, requires_grad=True)
+    out = ops.fused_exp_action(None, v1, F, L)
+    g = torch.randn_like(out)
+    out.backward(g)
+    v2 = v1.detach().clone().requires_grad_(True)
+    F2 = F.detach().clone().requires_grad_(True)
+    ref = lt.block_wigner_matrix_multiply(lt.group_matrix_to_eazyz(lt.rodrigues(v2)), F2.expand(1, -1, -1), L)
+    ref.backward(g)
+    assert_normwise(host(out.detach()), host(ref.detach()), tol=1e-5, what="n=1 out")
+    assert_normwise(host(F.grad)[None], host(F2.grad)[None], tol=1e-4, what="n=1 gF")
+    assert_normwise(host(v1.grad), host(v2.grad), tol=1e-3, what="n=1 gv")
+
+
 def test_bad_sizes_raise(gpu_device):
     import lie_vae.lie_tools as lt
     from lie_vae._lib import LieVaeHipError
