@@ -35,6 +35,10 @@ constexpr int kBwdVarJit = 1;  // ActionBwdArgs::variant: row-pair reads of F an
 // one-group blocks' post-chain slab pass (A/B): flat element list over the wave's degrees
 // (else one pass set per degree), and write-through (sc1) slab stores (else plain)
 constexpr int kBwdVarSlabFlat = 2, kBwdVarSlabWT = 4;
+// one-group compile-time-C blocks: the barrier after the prologue split in two, so each
+// wave's first (largest) degree computes its forward recompute P1..P4 -- which needs the
+// multiples and the spectrum, not the gradient tile -- while the tile's LDS-DMA is in flight
+constexpr int kBwdVarSplit = 8;
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
@@ -255,6 +259,27 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   const int fstr = CT > 0 ? nthr : 64;
   const int fbase = CT > 0 ? tid : lane;
   const float* fsrc = a.F + (CT > 0 ? 0 : rows_lo * C);
+  // Degrees walked largest first (every instantiation, so that all spectrum modes and the
+  // looping kernel add a sample's angle-gradient partials in the same order); kDesc: the
+  // one-group compile-time-C kernel also loads its prologue inputs ahead of the tile DMA
+  // and may split the prologue barrier (kBwdVarSplit: the largest degree's forward
+  // recompute overlapping the tile DMA)
+  constexpr bool kDesc = CT > 0 && !LOOP && FM == kBwdFShared;
+  const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
+  const int jt = tid / 3, q = tid - 3 * (tid / 3);
+  // kDesc: the prologue's angle and the VJP tail's v / mu loaded before the spectrum, so
+  // the spectrum staging's wait covers them and nothing after the tile DMA waits in vmcnt
+  // order behind it
+  float ang0 = 0.f, vmu0 = 0.f;
+  if constexpr (kDesc) {
+    const int64_t s0e = (int64_t)blockIdx.x * Sw;
+    const int Sve = (int)min((int64_t)Sw, a.n - s0e);
+    if (task) ang0 = a.ang[(s0e + min(jt, Sve - 1)) * 3 + (a.transpose ? 2 - q : q)];
+    if (a.v && tid < 12 * Sve && 12 * Sve <= nthr) {  // else the loop after the DMA
+      const int js = tid / 12, k = tid - 12 * js;
+      vmu0 = k < 3 ? a.v[(s0e + js) * 3 + k] : (a.mu ? a.mu[(s0e + js) * 9 + (k - 3)] : 0.f);
+    }
+  }
   if constexpr (GSLAB) {
     each_degree([&](int l) {  // this wave's rows
       for (int e = lane; e < (2 * l + 1) * C; e += 64) slab_at(l * l * C + e) = 0.f;
@@ -304,8 +329,6 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   float* vmu = Fbase + fsize;
   const float* Fl = GSLAB ? a.F + c : (CT > 0 ? Fw + c : Fw + c * frows - rows_lo);
   const int fstep = (GSLAB || CT > 0) ? C : 1;
-  const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
-  const int jt = tid / 3, q = tid - 3 * (tid / 3);
 
   phase_stamp(a.stamps, wave, 0);
   for (int64_t g = blockIdx.x; g < a.groups; g += LOOP ? gridDim.x : a.groups) {
@@ -342,20 +365,26 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
       // only this slot's angle (transpose: slot q takes angle 2 - q, sine negated)
       float cq, sq;
-      sincosf(a.ang[st * 3 + (a.transpose ? 2 - q : q)], &sq, &cq);
+      if constexpr (kDesc) (void)st;
+      sincosf(kDesc ? ang0 : a.ang[st * 3 + (a.transpose ? 2 - q : q)], &sq, &cq);
       if (a.transpose) sq = -sq;
       trig_row_fill1<LT>(trig + jt * kRow, cq, sq, q, LT);
     }
-    if (a.v) {  // v (3) and mu (9) of the group's samples for the VJP tail (12 * Sv may
-                // exceed the block: 252 values at C = 3)
+    if (kDesc && a.v && 12 * Sv <= nthr) {
+      if (tid < 12 * Sv) vmu[tid] = vmu0;
+    } else if (a.v) {  // v (3) and mu (9) of the group's samples for the VJP tail (12 * Sv
+                       // may exceed the block: 252 values at C = 3)
       for (int t = tid; t < 12 * Sv; t += nthr) {
         const int js = t / 12, k = t - 12 * js;
         if (k < 3) vmu[js * 12 + k] = a.v[(s0 + js) * 3 + k];
         else if (a.mu) vmu[js * 12 + k] = a.mu[(s0 + js) * 9 + (k - 3)];
       }
     }
-    // 3. the LDS-DMA writes of this wave have landed (an LDS-DMA is counted in vmcnt)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // 3. the LDS-DMA writes of this wave have landed (an LDS-DMA is counted in vmcnt);
+    //    kBwdVarSplit: only the multiples, the spectrum and v / mu here (LDS writes), the
+    //    tile after the first degree's forward recompute
+    bool split_pending = kDesc && (a.variant & kBwdVarSplit) != 0;
+    if (!split_pending) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     block_sync_lds();
     phase_stamp(a.stamps, wave, 1);
 
@@ -365,7 +394,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     const float* Fs = a.F + (s0 + min(j, Sv - 1)) * a.Fstride + c;  // per-sample spectrum
     float ga = 0.f, gb = 0.f, gc = 0.f;
     sfor<LT + 1>([&](auto Lc) {
-      constexpr int l = LV_CV(Lc);
+      constexpr int l = LT - LV_CV(Lc);
       if ((dmask >> l) & 1u) {
         constexpr int nn = 2 * l + 1;
         constexpr int r0 = l * l;
@@ -387,6 +416,11 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         jmul<l>(u, p2);                           // P2
         xm<l>(mult_lds<l, 1, LT>(tj), p2, u);     // P3
         jmul<l>(u, p4);                           // P4
+        if (split_pending) {  // the wave's first degree: now the tile
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          block_sync_lds();
+          split_pending = false;
+        }
         if constexpr (JIT) {
           xm_mem<l, true>(mult_lds<l, 0, LT>(tj), tile_lane + r0 * C, C, u);  // Q4
         } else {
@@ -437,6 +471,10 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
         if (a.stamps) degree_stamp(a.stamps, wave, l);
       }
     });
+    if (split_pending) {  // a wave without degrees still takes the tile barrier
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      block_sync_lds();
+    }
     phase_stamp(a.stamps, wave, 2);
     if constexpr (FM == kBwdFShared && !LOOP) {
       // one group per block: this wave's rows of the slab are the group's dF rows summed
