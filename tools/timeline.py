@@ -41,12 +41,15 @@ def stamps(lib, with_deg=False):
 
 def degree_costs(name, st, deg, nblk, masks):
     """Median time per degree (us): stamp at the end of degree l minus the end of the
-    wave's previous degree (phase-1 stamp for its first)."""
+    wave's previous degree (phase-1 stamp for its first), in the order the wave ran them
+    (the backward walks its degrees largest first, the forward smallest first)."""
     nb = min(nblk, DEG_BLOCKS)
     res = {}
     for w, m in enumerate(masks):
         prev = st[:nb, w, 1]
-        for l in [b for b in range(24) if (m >> b) & 1]:
+        ls = [b for b in range(24) if (m >> b) & 1]
+        ls.sort(key=lambda b: float(np.median(deg[:nb, w, b])))  # execution order
+        for l in ls:
             d = (deg[:nb, w, l] - prev) * TICK_US
             res[l] = (w, float(np.median(d)))
             prev = deg[:nb, w, l]
