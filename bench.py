@@ -19,6 +19,12 @@ Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §6):
   cpu_baseline     the CPU oracle (reference op sequence, torch CPU) on a bounded
                    sample: all usable cores + 1 thread, forward and forward+backward
   fwd_bwd          the training direction on the GPU (fused forward + backward kernels)
+  config5          BASELINE config 5 on every rank: l = 20, B = 8192 per GPU, bf16 out
+                   (fp32 recursion), HBM and fp32-VALU roofline fractions
+  train_step       BASELINE config 3 (N = 1: B = 512) / config 4 (N > 1: 512 per rank,
+                   RCCL bucketed all-reduce of the gradients): the full VAE training step
+                   (unsupervised.py:108-117) at reference precision (fp32) and with bf16
+                   autocast, samples/s of the whole job, max over ranks
 """
 import argparse
 import ctypes
@@ -36,6 +42,7 @@ sys.path.insert(0, REPO)
 from lie_vae.experiments import launch  # noqa: E402  (imports torch only; no HIP call)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 via v_pk_fma_f32 (= fp32 MFMA)
 SCRUB_BYTES = 512 << 20  # > 256 MiB Infinity Cache (MI355X_MICROARCH.md:40)
 
 
@@ -65,6 +72,11 @@ def parse():
     ap.add_argument("--sweep", default="16384,65536",
                     help="comma-separated batches also timed (HIP events, median of 3 rounds); "
                          "'' to skip")
+    ap.add_argument("--config5-launches", type=int, default=200,
+                    help="config-5 record: launches timed per round (0: skip the record)")
+    ap.add_argument("--train-steps", type=int, default=10,
+                    help="train_step record: timed steps per precision (0: skip the record)")
+    ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--dry-run", action="store_true",
                     help="rehearse the rank plumbing on CPU (gloo, no HIP call)")
     return ap.parse_args()
@@ -189,14 +201,18 @@ def main():
     v = torch.randn(B, 3, generator=g).to(dev)
     F = torch.randn(M, C, generator=g).to(dev)
     out = torch.empty(B, M, C, device=dev, dtype=out_dtype)
+    # the product operator's instantiation writes the angles too (torch_ops.cpp,
+    # lie_vae/_ops.py): the timed launches do the same (49 KB; not credited in the bytes)
+    ang_buf = torch.empty(B, 3, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
-    def launch_k(k, s=sp, o=None, vv=None, nb=B):
+    def launch_k(k, s=sp, o=None, vv=None, nb=B, a=None):
         o = out if o is None else o
         vv = v if vv is None else vv
-        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(vv), P(F), 0, P(o), dt, None, nb, L, C,
+        a = ang_buf if a is None else a
+        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(vv), P(F), 0, P(o), dt, P(a), nb, L, C,
                                                 0, k, s)
         if rc:
             raise RuntimeError(_lib.last_error())
@@ -355,6 +371,7 @@ def main():
         for nb in sweep_batches:
             vv = torch.randn(nb, 3, device=dev)
             oo = torch.empty(nb, M, C, device=dev, dtype=out_dtype)
+            aa = torch.empty(nb, 3, device=dev)
             # >= ~10 ms of launches per round: the first rounds after a fresh output
             # allocation run up to 30% slow (tools/sweep_dist.py), so one untimed round,
             # then the median of three
@@ -363,7 +380,7 @@ def main():
             for it in range(4):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                launch_k(reps, o=oo, vv=vv, nb=nb)
+                launch_k(reps, o=oo, vv=vv, nb=nb, a=aa)
                 e1.record(stream)
                 torch.cuda.synchronize(dev)
                 if it:
@@ -371,13 +388,14 @@ def main():
             t = sorted(ts)[1]
             gbs = algorithmic_bytes(nb, L, C, out_bytes) / t / 1e9
             sweep.append({"batch": nb, "us": t * 1e6, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS})
-            del vv, oo
+            del vv, oo, aa
 
     # independent batches on parallel streams (same kernel): aggregate throughput
     multi = None
     if args.launch == "graph" and args.multistream > 1:
         ms = args.multistream
         mouts = [torch.empty(B, M, C, device=dev, dtype=out_dtype) for _ in range(ms)]
+        mangs = [torch.empty(B, 3, device=dev) for _ in range(ms)]
         side = [torch.cuda.Stream(dev) for _ in range(ms)]
         mchunk = max(ms, chunk - chunk % ms)
         g2 = torch.cuda.CUDAGraph()
@@ -386,8 +404,8 @@ def main():
         with torch.cuda.graph(g2, stream=s2):
             for t in side:
                 t.wait_stream(s2)
-            for t, o in zip(side, mouts):
-                launch_k(mchunk // ms, ctypes.c_void_p(t.cuda_stream), o)
+            for t, o, a in zip(side, mouts, mangs):
+                launch_k(mchunk // ms, ctypes.c_void_p(t.cuda_stream), o, a=a)
             for t in side:
                 s2.wait_stream(t)
         reps = max(1, args.steps // mchunk)
@@ -402,7 +420,7 @@ def main():
         multi = {"streams": ms, "steps": reps * mchunk, "value": reps * mchunk * B * world / el2,
                  "unit": "samples/s", "us_per_step": el2 / (reps * mchunk) * 1e6,
                  "aggregate_GBs": abytes * reps * mchunk / el2 / 1e9}
-        del mouts
+        del mouts, mangs
 
     cache_cold = cold(args.cold_launches) if args.cold_launches > 0 and rank == 0 else None
 
@@ -427,6 +445,15 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(L, C, B, args.cpu_seconds)
+
+    # BASELINE configs 5 and 3 / 4 as bounded sub-records of the same line (every rank
+    # takes part: they are timed max over ranks like the headline)
+    config5 = None
+    if args.config5_launches > 0:
+        config5 = bench_config5(lib, dev, stream, world, rank, args.config5_launches)
+    train = None
+    if args.train_steps > 0:
+        train = bench_train_step(dev, env, args.train_steps, args.train_warmup)
 
     if rank == 0:
         rec = {
@@ -462,16 +489,118 @@ def main():
                                             "submission cost both brackets hold cancels. The "
                                             "raw t_K / K is us_per_launch_events_raw",
                          "events": "graph nodes" if events_in_graph else "stream",
+                         "instantiation": "product (angles written, as torch.ops.lievae."
+                                          "fused_exp_action)",
                          "cache": "hot (back-to-back launches)"},
             "cache_cold": cache_cold,
             "cpu_baseline": cpu,
             "fwd_bwd": fwd_bwd,
             "multistream": multi,
             "sweep": sweep,
+            "config5": config5,
+            "train_step": train,
         }
         print(json.dumps(rec), flush=True)
     if td:
         td.destroy_process_group()
+
+
+def bench_config5(lib, dev, stream, world, rank, launches, L=20, C=10, B=8192):
+    """BASELINE config 5: the fused exp -> ZYZ -> Wigner-D action at l = 20, B = 8192 per
+    GPU, bf16 output with fp32 recursion (lv_fused_exp_action_fwd, dtype bf16, writing the
+    angles as the product operator does).  Every rank times `launches` back-to-back launches
+    (HIP events on the launch stream, median of 3 rounds after an untimed one); the barrier
+    brackets the rounds and the value is all ranks' samples / the max-over-ranks time.
+    Roofline: HBM on the algorithmic bytes (72,369,384 B per launch) and
+    fp32 VALU on the D·F FLOPs (2·C·S_D = 246,820 per sample; the recursion's FLOPs are
+    implementation-dependent and not credited)."""
+    import torch.distributed as dist
+    M = (L + 1) ** 2
+    S_D = (L + 1) * (2 * L + 1) * (2 * L + 3) // 3
+    g = torch.Generator(device="cpu").manual_seed(5000 + rank)
+    v = torch.randn(B, 3, generator=g).to(dev)
+    F = torch.randn(M, C, generator=g).to(dev)
+    out = torch.empty(B, M, C, device=dev, dtype=torch.bfloat16)
+    ang = torch.empty(B, 3, device=dev)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def run(k):
+        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(v), P(F), 0, P(out), 1, P(ang), B, L, C,
+                                                0, k, sp)
+        if rc:
+            raise RuntimeError("lv_fused_exp_action_fwd (config 5) failed")
+
+    run(2)
+    torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    ts = []
+    for it in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        run(launches)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        if it:
+            ts.append(e0.elapsed_time(e1) / 1e3 / launches)
+    if dist.is_initialized():
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    us = sorted(ts)[1] * 1e6
+    us_max = max(ts) * 1e6
+    from lie_vae.experiments import launch as _launch
+    us_all = _launch.max_over_ranks(us, dev)
+    abytes = algorithmic_bytes(B, L, C, 2)
+    flops = 2 * C * S_D * B
+    hbm = abytes / (us_all * 1e-6) / 1e9
+    tf = flops / (us_all * 1e-6) / 1e12
+    return {"workload": "config5: fused exp -> ZYZ -> block Wigner-D action, l=20, C=10, "
+                        "B=8192 per GPU, bf16 out, fp32 recursion and angles",
+            "value": B * world / (us_all * 1e-6), "unit": "samples/s", "n_gpus": world,
+            "us_per_launch": us_all, "us_per_launch_rank0_median": us, "us_rank0_worst": us_max,
+            "launches_per_round": launches, "rounds_timed": 3, "wall_s": wall,
+            "timing": "HIP events around `launches` back-to-back launches on the launch "
+                      "stream, median of 3 rounds, max over ranks",
+            "roofline_hbm": {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": hbm / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": abytes},
+            "roofline_valu_f32": {"achieved": tf, "peak": F32_VALU_PEAK_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": tf / F32_VALU_PEAK_TFLOPS,
+                                  "flops_per_launch": flops,
+                                  "flops_note": "D·F only, 2·C·S_D per sample (S_D = 12,341)"}}
+
+
+def bench_train_step(dev, env, steps, warmup):
+    """BASELINE config 3 (N = 1: batch 512) and config 4 (N > 1: 512 per rank, the global
+    batch 512·N, RCCL bucketed all-reduce of the fp32 gradients, global-norm clip, Adam):
+    the reference's training step (unsupervised.py:108-117, VAE so3 / action, l = 10,
+    C = 10, deconv_hidden 200, s2s2 mean, batch norm, RGB 64x64) on synthetic x ~ U[0,1)
+    resident in HBM and random-init weights.  Twice: at the reference's fp32 and with bf16
+    autocast on the conv / linear layers (channels-last; the SO(3) kernels stay fp32).
+    MIOpen runs in immediate mode (no find: heuristic solutions), as a fresh box does."""
+    import bench_train
+    from lie_vae.experiments.vae import VAE
+    torch.backends.cudnn.benchmark = False
+    recs = {}
+    t0 = time.perf_counter()
+    for tag, amp, cl in (("f32", "off", False), ("bf16", "bf16", True)):
+        torch.manual_seed(0)
+        model = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10,
+                    rgb=True, batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(dev)
+        if cl:
+            model = model.to(memory_format=torch.channels_last)
+        rec = bench_train.time_train_steps(model, dev, env.world, env.rank, 512 * env.world,
+                                           steps, warmup, amp=amp)
+        rec["config"]["channels_last"] = cl
+        recs[tag] = rec
+        del model
+        torch.cuda.empty_cache()
+    recs["workload"] = (("config4: " if env.world > 1 else "config3: ") +
+                        "full sphere-cube VAE training step, 512 images per GPU")
+    recs["wall_s"] = time.perf_counter() - t0
+    recs["data"] = "synthetic x ~ U[0,1)^(512x3x64x64) per rank (seeded), random-init weights"
+    return recs
 
 
 def bench_fwd_bwd(v, F, L, dev, stream, iters=200):

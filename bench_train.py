@@ -102,7 +102,6 @@ def main():
     torch.cuda.set_device(dev)
 
     from lie_vae.experiments import nets
-    from lie_vae.experiments.train_dp import DPTrainer, param_count
     from lie_vae.experiments.vae import VAE
     nets.GEMM_LAYERS = args.conv_gemm == "on"
     nets.MFMA_DECONV = args.deconv == "mfma"
@@ -117,56 +116,78 @@ def main():
         model = model.to(memory_format=torch.channels_last)
     if args.iwae:
         return bench_iwae(args, model, env, dev)
+    rec = time_train_steps(model, dev, world, rank, args.global_batch, args.steps, args.warmup,
+                           amp=args.amp, graph=args.graph, fused_adam=args.adam == "fused")
+    if rank == 0:
+        rec["config"].update({"l_max": args.lmax, "deconv_hidden": args.deconv_hidden,
+                              "mean_mode": args.mean_mode, "channels_last": args.channels_last,
+                              "miopen_find": args.find, "conv_gemm": args.conv_gemm,
+                              "deconv": args.deconv, "fused_relu": args.fused_relu,
+                              "conv_dgrad": args.conv_dgrad, "adam": args.adam})
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def time_train_steps(model, dev, world, rank, global_batch, steps, warmup, amp="off",
+                     graph=False, fused_adam=True, flops=True):
+    """Time `steps` DPTrainer steps (elbo fwd + bwd + bucketed all-reduce at world > 1 +
+    global clip + Adam) on a synthetic per-rank shard after `warmup` steps; barrier +
+    synchronize on both sides, max over ranks.  Returns the record (rank 0 prints it)."""
+    import torch.distributed as dist
+    from lie_vae.experiments.train_dp import DPTrainer, param_count
     trainer = DPTrainer(model, lr=1e-3, clip_grads=1e-5,
-                        amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
-                        graph=args.graph, fused_adam=args.adam == "fused")
-    B = args.global_batch // world
+                        amp_dtype=torch.bfloat16 if amp == "bf16" else None,
+                        graph=graph, fused_adam=fused_adam)
+    B = global_batch // world
     g = torch.Generator(device="cpu").manual_seed(100 + rank)
     x = torch.rand(B, 3, 64, 64, generator=g).to(dev)
-
-    for _ in range(args.warmup):
+    t_setup = time.perf_counter()
+    for _ in range(warmup):
         trainer.step(x)
-    # model FLOPs of one step (forward + backward, counted per aten op: the convs,
-    # deconvs and linear layers; the SO(3) kernels are custom ops and not counted)
-    from torch.utils.flop_counter import FlopCounterMode
-    with FlopCounterMode(display=False) as fc:
-        trainer.step(x)
-    step_flops = fc.get_total_flops()
-    run = trainer.capture(x) if args.graph else (lambda: trainer.step(x))
+    step_flops = None
+    if flops:
+        # model FLOPs of one step (forward + backward, counted per aten op: the convs,
+        # deconvs and linear layers; the SO(3) kernels are custom ops and not counted)
+        from torch.utils.flop_counter import FlopCounterMode
+        with FlopCounterMode(display=False) as fc:
+            trainer.step(x)
+        step_flops = fc.get_total_flops()
+    run = trainer.capture(x) if graph else (lambda: trainer.step(x))
     torch.cuda.synchronize(dev)
+    warm_s = time.perf_counter() - t_setup
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss, recon, kl = run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     el = launch.max_over_ranks(time.perf_counter() - t0, dev)
-    peak = F32_PEAK_TFLOPS if args.amp == "off" else BF16_PEAK_TFLOPS
-    if rank == 0:
-        print(json.dumps({
-            "metric": "VAE train samples/s (conv enc + SO(3) reparam + action dec, l=10)",
-            "value": args.global_batch * args.steps / el, "unit": "samples/s", "n_gpus": world,
-            "steps": args.steps, "ms_per_step": el * 1e3 / args.steps,
-            "config": {"global_batch": args.global_batch, "per_gpu": B, "l_max": args.lmax,
-                       "deconv_hidden": args.deconv_hidden, "mean_mode": args.mean_mode,
-                       "params": param_count(model),
-                       "dtype": "f32" if args.amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
-                       "channels_last": args.channels_last, "miopen_find": args.find,
-                       "conv_gemm": args.conv_gemm,
-                       "deconv": args.deconv, "fused_relu": args.fused_relu, "conv_dgrad": args.conv_dgrad, "adam": args.adam,
-                       "launch": "graph" if args.graph else "eager"},
-            "matrix": {"flops_per_step_per_gpu": step_flops,
-                       "achieved_tflops_per_gpu": step_flops / (el / args.steps) / 1e12,
-                       "peak_tflops": peak,
-                       "frac": step_flops / (el / args.steps) / 1e12 / peak},
-            "loss": float(loss.item()), "recon": float(recon.mean().item()),
-            "kl": float(kl.mean().item())}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    nranks = launch.ranks_seen(dev)
+    peak = F32_PEAK_TFLOPS if amp == "off" else BF16_PEAK_TFLOPS
+    rec = {
+        "metric": "VAE train samples/s (conv enc + SO(3) reparam + action dec, l=10)",
+        "value": global_batch * steps / el, "unit": "samples/s", "n_gpus": world,
+        "ranks_seen": nranks, "max_over_ranks": world > 1,
+        "steps": steps, "warmup": warmup, "ms_per_step": el * 1e3 / steps,
+        "warmup_s": warm_s,
+        "config": {"global_batch": global_batch, "per_gpu": B, "params": param_count(model),
+                   "dtype": "f32" if amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
+                   "parallelism": (f"dp{world}: RCCL bucketed all-reduce of fp32 gradients"
+                                   if world > 1 else "single GPU"),
+                   "launch": "graph" if graph else "eager"},
+        "loss": float(loss.item()), "recon": float(recon.mean().item()),
+        "kl": float(kl.mean().item())}
+    if step_flops is not None:
+        rec["matrix"] = {"flops_per_step_per_gpu": step_flops,
+                         "achieved_tflops_per_gpu": step_flops / (el / steps) / 1e12,
+                         "peak_tflops": peak,
+                         "frac": step_flops / (el / steps) / 1e12 / peak}
+    return rec
 
 
 def bench_iwae(args, model, env, dev):

@@ -22,6 +22,9 @@
 // step's MFMAs run, then written to the other LDS buffer (row pitch 80 B: the 16-byte
 // fragment reads of 8 consecutive rows fall in distinct banks).  Epilogue: + bias, round
 // to bf16, stage the tile in LDS, 16-byte stores of whole 2·Cout-byte output rows.
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <algorithm>
 
 #include "lv_common.h"
@@ -1140,19 +1143,27 @@ int lv_deconv4s2_small_pack_dgrad_weight_bf16(const void* w, void* wd, int Cin, 
 constexpr int kWgMaxBlocks = 512;  // wgrad partial slabs (workspace bound)
 static int small_wgrad_blocks(int64_t ntiles) { return (int)std::min<int64_t>(ntiles, kWgMaxBlocks); }
 
-// resident blocks of a persistent kernel on this device (all CUs x its occupancy), cached
+// resident blocks of a persistent kernel on the current device (all CUs x its
+// occupancy), cached per (device, kernel, threads, LDS bytes) under a mutex: launches may
+// come from several host threads and devices
 static int resident_blocks(const void* kern, int threads, size_t lds) {
-  static const void* keys[16];
-  static int vals[16];
-  static int used = 0;
-  for (int i = 0; i < used; ++i)
-    if (keys[i] == kern) return vals[i];
-  int per_cu = 0, dev = 0, cus = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, int, size_t>, int> cache;
+  const auto key = std::make_tuple(dev, kern, threads, lds);
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) per_cu = 1;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+  if (dev < 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
   const int v = std::max(1, per_cu) * std::max(1, cus);
-  if (used < 16) { keys[used] = kern; vals[used] = v; ++used; }
+  std::lock_guard<std::mutex> lock(mu);
+  cache[key] = v;
   return v;
 }
 

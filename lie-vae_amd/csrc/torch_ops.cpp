@@ -12,8 +12,11 @@
 #include <c10/hip/HIPGraphsC10Utils.h>
 #include <c10/hip/HIPStream.h>
 
+#include <c10/core/DeviceGuard.h>
+
+#include <map>
 #include <mutex>
-#include <unordered_map>
+#include <utility>
 
 #include "../../include/lievae.h"
 
@@ -40,11 +43,12 @@ Tensor workspace(int64_t n, int64_t L, int64_t C, const Tensor& like, void* stre
   auto opts = like.options().dtype(torch::kUInt8);
   if (c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None)
     return torch::empty({nb}, opts);
+  // keyed by (device, stream): the default stream's handle is the same on every device
   static std::mutex mu;
-  static std::unordered_map<void*, Tensor> cache;
+  static std::map<std::pair<int, void*>, Tensor> cache;
   std::lock_guard<std::mutex> lock(mu);
-  Tensor& buf = cache[stream];
-  if (!buf.defined() || buf.numel() < nb || buf.device() != like.device())
+  Tensor& buf = cache[{(int)like.device().index(), stream}];
+  if (!buf.defined() || buf.numel() < nb)
     buf = torch::empty({std::max<int64_t>(nb, 1 << 20)}, opts);
   return buf;
 }
@@ -52,7 +56,15 @@ Tensor workspace(int64_t n, int64_t L, int64_t C, const Tensor& like, void* stre
 struct FusedExpAction : public torch::autograd::Function<FusedExpAction> {
   static Tensor forward(AutogradContext* ctx, const std::optional<Tensor>& mu, const Tensor& v,
                         const Tensor& spec, int64_t L, bool transpose, bool out_bf16) {
-    TORCH_CHECK(v.is_cuda() && spec.is_cuda(), "lievae::fused_exp_action: device tensors only (no CPU fallback)");
+    // every input on ONE HIP device: the kernels take raw device pointers, so a CPU tensor
+    // or a tensor of another GPU must be refused here, before any launch
+    TORCH_CHECK(v.is_cuda() && spec.is_cuda() && (!mu.has_value() || !mu->defined() || mu->is_cuda()),
+                "lievae::fused_exp_action: device tensors only (no CPU fallback)");
+    TORCH_CHECK(spec.device() == v.device() && (!mu.has_value() || !mu->defined() || mu->device() == v.device()),
+                "lievae::fused_exp_action: mu, v and spectrum must be on one device (got v on ", v.device(),
+                ", spectrum on ", spec.device(), mu.has_value() && mu->defined() ? ", mu on " : "",
+                mu.has_value() && mu->defined() ? mu->device().str() : std::string(), ")");
+    const c10::DeviceGuard guard(v.device());
     TORCH_CHECK(v.dim() == 2 && v.size(1) == 3, "v must be (n,3)");
     TORCH_CHECK(spec.dim() == 2 && spec.size(0) == (L + 1) * (L + 1), "spectrum must be ((L+1)^2, C)");
     const Tensor vc = v.scalar_type() == torch::kFloat32 && v.is_contiguous() ? v : v.to(torch::kFloat32).contiguous();
@@ -90,7 +102,10 @@ struct FusedExpAction : public torch::autograd::Function<FusedExpAction> {
     const Tensor& ang = saved[3];
     const int64_t L = ctx->saved_data["L"].toInt();
     const bool transpose = ctx->saved_data["transpose"].toBool();
+    const c10::DeviceGuard guard(v.device());
     Tensor g = grads[0];
+    TORCH_CHECK(g.device() == v.device(), "lievae::fused_exp_action backward: gradient on ", g.device(),
+                ", inputs on ", v.device());
     g = g.scalar_type() == torch::kFloat32 && g.is_contiguous() ? g : g.to(torch::kFloat32).contiguous();
     const int64_t n = v.size(0), C = spec.size(1);
     auto gspec = torch::empty_like(spec);

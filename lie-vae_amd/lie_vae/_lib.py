@@ -167,8 +167,14 @@ def load_torch_ops():
         _torch_ops = False
         if os.path.exists(TORCH_OPS_PATH):
             load()  # the kernels' library first (the operators link against it)
-            torch.ops.load_library(TORCH_OPS_PATH)
-            _torch_ops = True
+            try:
+                torch.ops.load_library(TORCH_OPS_PATH)
+                _torch_ops = True
+            except (OSError, RuntimeError) as e:  # stale build / torch ABI changed
+                import warnings
+                warnings.warn(f"lie_vae: {TORCH_OPS_PATH} did not load ({e}); the fused op "
+                              "runs through the Python autograd path (same kernels). Rebuild "
+                              "with `make -C lie-vae_amd/csrc`.")
     return _torch_ops
 
 
@@ -187,9 +193,18 @@ def ptr(t):
 
 
 def require_device(*tensors):
-    """The HIP path only: refuse CPU tensors loudly instead of silently falling back."""
+    """The HIP path only: refuse CPU tensors loudly instead of silently falling back, and
+    tensors spread over several GPUs (the kernels take raw pointers of one device)."""
+    dev = None
     for t in tensors:
-        if t is not None and not t.is_cuda:
+        if t is None:
+            continue
+        if not t.is_cuda:
             raise RuntimeError(
                 "lie_vae ops run only on the MI355X HIP path (got a CPU tensor); "
                 "move inputs to a cuda:N (HIP) device. There is no CPU fallback.")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"lie_vae ops need all inputs on one device (got {dev} and "
+                               f"{t.device})")

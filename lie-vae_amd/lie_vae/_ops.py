@@ -272,11 +272,20 @@ def _check_spectrum(spectrum, n, L, what):
     return spectrum
 
 
+def _check_out_dtype(out_dtype, what):
+    """The kernels write fp32 or bf16 output only; anything else would be written with
+    the wrong element size (checked before either path, Python or C++ operator)."""
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"{what}: out_dtype must be torch.float32 or torch.bfloat16, "
+                         f"got {out_dtype}")
+
+
 def group_action(angles, spectrum, L, transpose=False, out_dtype=F32):
     """block_wigner_matrix_multiply on the HIP path; angles (n,3), spectrum (M,C),
     (n,M,C) or a stride-0 expand of (M,C)."""
     assert angles.dim() == 2 and angles.shape[1] == 3, \
         f"angles must be (n,3), got {tuple(angles.shape)}"
+    _check_out_dtype(out_dtype, "group_action")
     spectrum = _check_spectrum(spectrum, angles.shape[0], L, "group_action")
     _lib.require_device(angles, spectrum)
     return _GroupAction.apply(angles, _contig(spectrum), L, transpose, out_dtype)
@@ -345,6 +354,7 @@ def fused_exp_action(mu, v, spectrum, L, transpose=False, out_dtype=F32):
     n = v.shape[0]
     if mu is not None:
         assert tuple(mu.shape) == (n, 3, 3), f"mu must be ({n},3,3), got {tuple(mu.shape)}"
+    _check_out_dtype(out_dtype, "fused_exp_action")
     spectrum = _check_spectrum(spectrum, n, L, "fused_exp_action")
     if spectrum.dim() != 2:
         raise ValueError("fused_exp_action takes a shared (M,C) spectrum; use group_action "

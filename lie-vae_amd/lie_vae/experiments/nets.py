@@ -40,9 +40,16 @@ class _CachedCast(torch.autograd.Function):
     gradient-bucket view of DPTrainer (``p._lv_grad_sink`` set by BucketedAllReduce), the
     bf16 gradient added into .grad in place by the library's one-pass kernel
     (lv_accumulate_bf16_f32; torch's mixed-dtype add_ runs a non-vectorised kernel, ~50 us
-    per conv weight) and the bucket's post-accumulate hook called directly: one kernel per
-    parameter instead of a cast and AccumulateGrad's add (22 + 22 tiny kernels per config-3
-    step)."""
+    per conv weight) and no gradient returned: one kernel per parameter instead of a cast
+    and AccumulateGrad's add (22 + 22 tiny kernels per config-3 step).
+
+    The bucket's accounting stays with the parameter's post-accumulate hook: autograd runs
+    a leaf's AccumulateGrad once per backward, after every path into it (this node's None
+    included), and fires the hook then -- so however many times the cached copy (or the
+    parameter directly) entered the graph, every contribution is in the bucket before its
+    hook counts the parameter, once.  (Round 4 also called the hook from here: with the
+    hook's own call that counted a parameter twice and could launch a bucket's all-reduce
+    early; BucketedAllReduce now refuses a second count in one step.)"""
 
     @staticmethod
     def forward(ctx, p, pb):
@@ -53,10 +60,9 @@ class _CachedCast(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         p = ctx.p
-        sink = getattr(p, "_lv_grad_sink", None)
         gr = p.grad
-        if sink is not None and gr is not None and not torch.is_grad_enabled():
-            if (g.dtype == torch.bfloat16 and gr.dtype == torch.float32 and g.shape == gr.shape
+        if getattr(p, "_lv_grad_sink", None) is not None and gr is not None and not torch.is_grad_enabled():
+            if (gr.is_cuda and g.dtype == torch.bfloat16 and gr.dtype == torch.float32 and g.shape == gr.shape
                     and g.stride() == gr.stride()
                     and (gr.is_contiguous() or (gr.dim() == 4 and gr.is_contiguous(memory_format=torch.channels_last)))):
                 from .. import _lib
@@ -64,7 +70,6 @@ class _CachedCast(torch.autograd.Function):
                           _lib.stream_of(gr.device))
             else:
                 gr.add_(g)
-            sink(p)
             return None, None
         return g.to(ctx.dt), None
 

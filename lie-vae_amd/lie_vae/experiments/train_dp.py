@@ -59,10 +59,19 @@ class BucketedAllReduce:
                 off += p.numel()
             self.state.append({"buf": buf, "left": len(plist), "handle": None})
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
-        for p in self.params:  # gradients that bypass AccumulateGrad (nets._CachedCast)
+        for p in self.params:  # .grad is a bucket view: nets._CachedCast may add into it
             p._lv_grad_sink = self._on_grad
+        self._seen = set()
 
     def _on_grad(self, p):
+        # once per parameter per step: a second call means a gradient arrived after its
+        # bucket may already be in flight (silently lost from the all-reduce), so refuse it
+        if p in self._seen:
+            raise RuntimeError(
+                "BucketedAllReduce: a parameter was counted twice in one step (a second "
+                "backward without zero_grad?); its bucket's all-reduce may already be in "
+                "flight.")
+        self._seen.add(p)
         st = self.state[self.owner[p]]
         st["left"] -= 1
         if st["left"] == 0:
@@ -78,6 +87,7 @@ class BucketedAllReduce:
             st["buf"].zero_()
             st["left"] = len(plist)
             st["handle"] = None
+        self._seen = set()
 
     def finish(self):
         """Wait for every bucket (launching any whose parameters got no gradient) and

@@ -135,3 +135,23 @@ def test_spectrum_shape_contract_raises():
     # a stride-0 expand of (M, C) is the shared form (and then hits the device check)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.fused_exp_action(None, torch.randn(6, 3), torch.randn(16, 2).expand(6, -1, -1), 3)
+
+
+def test_out_dtype_validated_before_any_path():
+    """an out_dtype other than fp32 / bf16 would be written with the wrong
+    element size by the kernels; both the Python and the C++ operator paths refuse it
+    up front (ValueError, before the device check)."""
+    from lie_vae import _ops
+    v = torch.randn(4, 3)
+    F = torch.randn(16, 2)
+    for dt in (torch.float16, torch.float64, torch.int32):
+        with pytest.raises(ValueError, match="out_dtype"):
+            _ops.fused_exp_action(None, v, F, 3, out_dtype=dt)
+        with pytest.raises(ValueError, match="out_dtype"):
+            _ops.group_action(torch.randn(4, 3), F, 3, out_dtype=dt)
+
+
+def test_require_device_refuses_cpu_and_mixed():
+    from lie_vae import _lib
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.require_device(None, torch.randn(2))

@@ -192,3 +192,33 @@ def test_capture_refuses_uncapturable_collective():
         for r in range(2):
             with open(os.path.join(d, f"cap{r}.txt")) as f:
                 assert "needs the nccl" in f.read()
+
+
+def test_cached_cast_sink_once_per_parameter():
+    """ADVICE r4 (nets._CachedCast): a parameter is counted by its bucket once per step,
+    after every contribution is in the bucket.  Used once or twice through its cached bf16
+    copy -- and beside a direct use -- the gradient lands in the bucket view and the
+    post-accumulate hook (which autograd fires once, after all paths into the leaf) counts
+    it once; a second count in one step raises instead of racing the bucket's
+    all-reduce."""
+    from lie_vae.experiments import nets
+    p = nn.Parameter(torch.randn(5))
+    ar = train_dp.BucketedAllReduce([p])
+    counted = []
+    ar._launch = lambda st: counted.append(torch.clone(p.grad))  # what the all-reduce would send
+    pb = p.detach().to(torch.bfloat16)
+    cases = [
+        (lambda: (nets._CachedCast.apply(p, pb).float() * 2).sum(), 2.0),
+        (lambda: (nets._CachedCast.apply(p, pb).float() * 2).sum()
+         + (nets._CachedCast.apply(p, pb).float() * 3).sum(), 5.0),
+        (lambda: (nets._CachedCast.apply(p, pb).float() * 2).sum() + (p * 4).sum(), 6.0),
+    ]
+    for make, want in cases:
+        ar.zero_grad()
+        counted.clear()
+        make().backward()
+        assert ar.state[0]["left"] == 0
+        assert len(counted) == 1, "bucket launched more or less than once"
+        assert torch.equal(counted[0], torch.full((5,), want)), (counted[0], want)
+        with pytest.raises(RuntimeError, match="counted twice"):
+            ar._on_grad(p)

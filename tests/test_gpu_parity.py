@@ -576,6 +576,31 @@ def test_fused_torch_operator_matches_python_function_bitwise(gpu_device):
     assert torch.equal(out_g, ref[0]) and torch.equal(v.grad, ref[1]) and torch.equal(F.grad, ref[2])
 
 
+def test_torch_operator_refuses_cpu_or_mixed_inputs(gpu_device):
+    """the operator INTEGRATION.md tells integrators to call directly
+    checks every input's device before any launch -- a CPU mean (or v / spectrum) raises a
+    clean RuntimeError instead of reaching the kernel as an invalid device pointer -- and
+    the Python entry point refuses an out_dtype the kernels cannot write."""
+    import lie_vae._ops as ops
+    import lie_vae.lie_tools as lt
+    assert ops._TORCH_OPS
+    n, L, C = 64, 3, 4
+    v = torch.randn(n, 3, device=gpu_device)
+    F = torch.randn((L + 1) ** 2, C, device=gpu_device)
+    mu = lt.random_group_matrices(n, device=gpu_device).contiguous()
+    for args in [(mu.cpu(), v, F), (mu, v.cpu(), F), (mu, v, F.cpu()), (None, v, F.cpu())]:
+        with pytest.raises(RuntimeError, match="device tensors only|one device"):
+            torch.ops.lievae.fused_exp_action(*args, L, False, False)
+        with pytest.raises(RuntimeError, match="CPU"):
+            ops.fused_exp_action(*args, L)
+    with pytest.raises(ValueError, match="out_dtype"):
+        ops.fused_exp_action(mu, v, F, L, out_dtype=torch.float16)
+    # the device stays usable after the refusals
+    out = torch.ops.lievae.fused_exp_action(mu, v, F, L, False, False)
+    torch.cuda.synchronize(gpu_device)
+    assert torch.isfinite(out).all()
+
+
 def test_fused_vs_oracle_config2(gpu_device):
     """Config 2 exactly: B=4096, l=10, C=10, v ~ N(0,1), shared F (no mu)."""
     import lie_vae._ops as ops

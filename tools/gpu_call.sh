@@ -84,7 +84,7 @@ for s in "$@"; do
       step pmc_bwd 900 bash tools/gpu_pmc_bwd.sh; cat "$OUT/pmc_bwd.log" ;;
     ab-c5)  # config-5 bf16 tile options (AB_C5 = the variant specs of tools/gpu_variants.sh)
       step ab_c5 900 bash tools/gpu_variants.sh "--lmax 20 --batch 8192 --dtype bf16 --sweep=65536" \
-        ${AB_C5:-base= pair=LV_TILE_BF16=1 alias=LV_TILE_BF16=4 both=LV_TILE_BF16=5 sw5=LV_TILE_SW=5 alias_sw5=LV_TILE_BF16=4,LV_TILE_SW=5}
+        ${AB_C5:-base= sw5=LV_TILE_SW=5}
       cat "$OUT/ab_c5.log" ;;
     ab-bwd)  # backward knob variants (AB_KNOBS, tools/bwd_reduce_ab.py) at AB_BATCHES
       step ab_bwd 900 env AB_KNOBS="${AB_KNOBS:-LV_BWD_REDUCE=0,LV_BWD_REDUCE=16,LV_BWD_REDUCE=3,LV_BWD_VARIANT=1,LV_BWD_REDUCE=0}" \

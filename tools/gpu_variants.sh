@@ -3,7 +3,7 @@
 # (tools/c5_hash.py: must match the first variant bit for bit where the arithmetic is the
 # same).  Usage:
 #   bash tools/gpu_variants.sh "<bench.py args>" tag=VAR=val,VAR=val tag2=... 
-# e.g. bash tools/gpu_variants.sh "--lmax 20 --batch 8192 --dtype bf16" base= pair=LV_TILE_BF16=1
+# e.g. bash tools/gpu_variants.sh "--lmax 20 --batch 8192 --dtype bf16" base= sw5=LV_TILE_SW=5
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/variants
