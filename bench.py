@@ -578,9 +578,12 @@ def bench_train_step(dev, env, steps, warmup):
     C = 10, deconv_hidden 200, s2s2 mean, batch norm, RGB 64x64) on synthetic x ~ U[0,1)
     resident in HBM and random-init weights.  Twice: at the reference's fp32 and with bf16
     autocast on the conv / linear layers (channels-last; the SO(3) kernels stay fp32).
-    MIOpen runs in immediate mode (no find: heuristic solutions), as a fresh box does."""
+    MIOpen runs in immediate mode (no find) off the package's find-db
+    (lie_vae/data/miopen, nets.use_packaged_miopen_db)."""
     import bench_train
+    from lie_vae.experiments import nets
     from lie_vae.experiments.vae import VAE
+    db = nets.use_packaged_miopen_db()
     torch.backends.cudnn.benchmark = False
     recs = {}
     t0 = time.perf_counter()
@@ -600,6 +603,8 @@ def bench_train_step(dev, env, steps, warmup):
                         "full sphere-cube VAE training step, 512 images per GPU")
     recs["wall_s"] = time.perf_counter() - t0
     recs["data"] = "synthetic x ~ U[0,1)^(512x3x64x64) per rank (seeded), random-init weights"
+    recs["miopen"] = ("immediate mode, find-db " + ("lie_vae/data/miopen (tools/gen_miopen_db.sh)"
+                                                    if db else "absent: fallback heuristics"))
     return recs
 
 

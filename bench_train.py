@@ -97,6 +97,9 @@ def main():
             dist.destroy_process_group()
         return
     torch.backends.cudnn.benchmark = args.find
+    if not args.find:  # immediate mode: off the package's find-db unless one is set
+        from lie_vae.experiments import nets as _nets
+        _nets.use_packaged_miopen_db()
     launch.init_process_group(env, "nccl")
     dev = torch.device("cuda", launch.device_index(env))
     torch.cuda.set_device(dev)

@@ -24,6 +24,30 @@ from torch.nn import functional as F
 GEMM_LAYERS = True
 
 
+def use_packaged_miopen_db():
+    """Point MIOpen at the find-db shipped with the package (lie_vae/data/miopen: MIOpen's
+    find results for the config-3 / config-4 convolutions on MI355X, gfx950 with 256 CUs,
+    made by tools/gen_miopen_db.sh), copied to a private temp directory because MIOpen
+    writes next to it.  Immediate mode (torch.backends.cudnn.benchmark = False) then runs
+    the recorded winners instead of its fallback heuristics, which pick ConvDirectNaive
+    kernels (30-300 ms per call) for several NHWC bf16 shapes.  Must run before the
+    process's first convolution; a MIOPEN_USER_DB_PATH already set is left alone.  Returns
+    the directory in use (None if the package has no db)."""
+    import os
+    import shutil
+    import tempfile
+    if os.environ.get("MIOPEN_USER_DB_PATH"):
+        return os.environ["MIOPEN_USER_DB_PATH"]
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "miopen")
+    if not os.path.isdir(src):
+        return None
+    dst = tempfile.mkdtemp(prefix="lievae_miopen_db_")
+    for f in os.listdir(src):
+        shutil.copy(os.path.join(src, f), dst)
+    os.environ["MIOPEN_USER_DB_PATH"] = dst
+    return dst
+
+
 def _cl(t):
     return t.dim() == 4 and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
 
