@@ -537,17 +537,46 @@ constexpr int64_t kBwdMaxBlocksFallback = 1024;
 
 struct BwdPlan {
   int Sw, nseg, gx, fpitch, fmode;
+  int persist;            // action_bwd_persist_kernel
+  size_t ws_gang_off;     // persist: byte offset of the angle-gradient region (fused VJP)
   int64_t groups;
   int seg_lo[kMaxSeg + 1];
   unsigned seg_mask[kMaxSeg];
   size_t lds, ws;
 };
 
+// Persistent backward (action_bwd_persist.h) from this many 6-sample groups up: 2 blocks
+// per CU walk the groups with the next group's gradient tile and multiples prefetched under
+// the current chain, one dF slab per block.  Below it the one-group kernel's single round
+// of blocks is shorter.
+constexpr int64_t kBwdPersistMinGroups = 1536;
+
 bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   static const int kEnvNseg = LV_KNOB("LV_BWD_NSEG", 0);      // A/B testing only
   static const int kEnvGlobal = LV_KNOB("LV_BWD_FGLOBAL", 0);  // force the fallback (tests)
+  static const int kEnvPersistMin = LV_KNOB("LV_BWD_PERSIST_MIN", (int)kBwdPersistMinGroups);  // A/B; 0 = off
   b = BwdPlan{};
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
+  if (sharedF && C == kTileFastC && L >= kBwdPersistWaves - 1 && L <= kBwdPersistMaxL && !kEnvGlobal &&
+      kEnvPersistMin > 0) {
+    const int Sw = 64 / C;
+    const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
+    if (groups >= kEnvPersistMin) {
+      b.persist = 1;
+      b.Sw = Sw;
+      b.nseg = kBwdPersistWaves;
+      b.fmode = kBwdFShared;
+      b.groups = groups;
+      b.gx = (int)std::min<int64_t>(groups, kBwdCUs * kBwdPersistBlocksPerCU);
+      plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
+      balance_masks(L, b.nseg, true, b.seg_mask);
+      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, kBwdPersistWaves);
+      const size_t slabs = sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk);
+      b.ws_gang_off = slabs;
+      b.ws = slabs + sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);
+      return true;
+    }
+  }
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, true);
   for (int fallback = (kEnvGlobal && sharedF) ? 1 : 0; fallback < 2; ++fallback) {
@@ -674,6 +703,21 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.fmode = b.fmode;
   p.lds = b.lds;
   p.stream = st;
+  p.persist = b.persist;
+  if (b.persist) {
+    // the persistent kernel writes the angle gradient (the fused path: into the workspace,
+    // then the per-sample exp -> ZYZ VJP below) and chunk-major slabs, one per block
+    p.a.slab_chunked = 1;
+    if (v) p.a.gang = reinterpret_cast<float*>(static_cast<char*>(workspace) + b.ws_gang_off);
+    p.a.v = nullptr;
+    p.a.mu = nullptr;
+    if (int e = kBwdRun[L](p)) return e;
+    hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
+                       (const float*)workspace, gF, MC, b.gx, p.a.stamps);
+    LV_CHECK_LAUNCH("action_bwd_reduce3_kernel");
+    if (v) return lv_exp_eazyz_vjp(mu, v, p.a.gang, gmu, gv, n, st);
+    return LV_OK;
+  }
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
   // dF slab reduce: chunk-major slabs + action_bwd_reduce3_kernel by default
@@ -789,7 +833,7 @@ int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* pla
   if (int e = check_common(n, L, C, LV_DTYPE_F32)) return e;
   BwdPlan b;
   LV_CHECK_ARG(plan_bwd(n, L, C, shared_F != 0, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
-  plan[0] = b.fmode;
+  plan[0] = b.persist ? 3 : b.fmode;
   plan[1] = b.gx;
   plan[2] = b.nseg;
   plan[3] = 64 * b.nseg;

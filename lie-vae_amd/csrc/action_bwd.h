@@ -605,12 +605,17 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
     each_degree([&](int l) { write_slab_rows(a, slabL, l * l * C, (2 * l + 1) * C, lane); });
 }
 
+}  // namespace lv
+#include "action_bwd_persist.h"
+namespace lv {
+
 // Slab count per block of action_bwd_reduce_kernel (defined in action.hip).
 constexpr int kBwdReduceWaves = 16;
 
 struct BwdLaunch {
   ActionBwdArgs a;
   int gx, nseg, fmode;
+  int persist;  // action_bwd_persist_kernel (large batches, C = 10, shared spectrum)
   size_t lds;
   hipStream_t stream;
 };
@@ -622,6 +627,11 @@ struct BwdLauncher {
 template <int LT>
 int BwdLauncher<LT>::run(BwdLaunch& p) {
   const dim3 grid(p.gx), block(64 * p.nseg);
+  if (p.persist) {
+    if constexpr (LT <= kBwdPersistMaxL)
+      hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves>), grid, block, p.lds, p.stream, p.a);
+    LV_RETURN_LAUNCH("action_bwd_persist_kernel");
+  }
   if (p.fmode == kBwdFSample)
     hipLaunchKernelGGL((action_bwd_tile_kernel<LT, 0, kBwdFSample>), grid, block, p.lds, p.stream, p.a);
   else if (p.fmode == kBwdFSharedGlobal)

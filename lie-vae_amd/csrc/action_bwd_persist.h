@@ -1,0 +1,253 @@
+#pragma once
+// Persistent group-action backward for large batches (compile-time C = 10, shared spectrum,
+// l_max <= kBwdPersistMaxL): the reference's autograd through lie_tools.py:211-253
+// (wigner_d_matrix, block_wigner_matrix_multiply) for the training direction.
+//
+// The one-group tile kernel (action_bwd.h) runs one 6-sample group per block, so every
+// block pays its whole phase chain -- gradient-tile load, prologue, chain, per-group dF slab
+// pass, angle barrier -- back to back, and writes one 4.8 KB dF slab per 6 samples (a
+// third of the gradient tile's bytes again at l = 10, read back by the reduce).  Beyond
+// 4,096 groups the grid was capped and blocks looped over groups in a 256-VGPR build.
+//
+// Here a grid of 2 blocks per CU walks the groups (block b: groups b, b + P, b + 2P, ...),
+// and each block overlaps group k's chain with group k+1's loads:
+//   * the gradient tile of group k+1 goes global -> LDS by LDS-DMA into the second of two
+//     tile buffers while the waves run group k's chain (no VGPR holds it in flight);
+//   * the prologue of group k+1 (sincos of the stored angle, multiples of one (sample,
+//     slot) per task lane, tasks spread over the block's waves) runs after each wave's
+//     chain, into the second of two multiples tables, its angle loads issued at the top;
+//   * each wave adds its degrees' dF rows, summed over the group's samples, into the
+//     block's LDS slab (its own rows only: no race); the slab leaves once per block;
+//   * ONE block barrier per group: it publishes the angle partials, the next tile and the
+//     next multiples, and frees the current buffers.
+// The chain itself (P1..P4 forward recompute, Q4..dF transposed chain, angle gradients as
+// <Q4, K P4>, <Q2, K P2>, <dF, K F>) is the one-group kernel's JIT chain, operation for
+// operation.  Summation orders are fixed by the plan (degree set per wave, groups per
+// block): reproducible bit for bit, and within fp32 rounding of the one-group kernel.
+// The angle gradient goes to a.gang (the caller's, or a workspace region for the fused
+// exp -> ZYZ VJP, which the host then runs as lv_exp_eazyz_vjp's kernel).
+// Included by action_bwd.h after the one-group kernel and its helpers.
+
+namespace lv {
+
+constexpr int kBwdPersistMaxL = 10;
+constexpr int kBwdPersistWaves = 4;      // degree-set waves per block
+constexpr int kBwdPersistBlocksPerCU = 2;
+
+// LDS floats of the persistent kernel: 2 tiles, 2 multiples tables, 2 angle-partial
+// buffers, the dF slab and the spectrum.
+__host__ __device__ constexpr int persist_tile_floats(int L) {
+  return (((64 / 10) * (L + 1) * (L + 1) * 10 * 4 + 16 + 15) & ~15) / 4;
+}
+__host__ __device__ constexpr int persist_lds_floats(int L, int NW) {
+  return 2 * persist_tile_floats(L) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
+         2 * ((((L + 1) * (L + 1) * 10) + 3) & ~3);
+}
+
+template <int LT, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
+void action_bwd_persist_kernel(ActionBwdArgs a) {
+  constexpr int C = kTileFastC;
+  constexpr int Sw = 64 / C;
+  constexpr int MC = (LT + 1) * (LT + 1) * C;
+  constexpr int MC4 = (MC + 3) & ~3;
+  constexpr int kRow = TrigLds<LT>::kRow;
+  constexpr int kTile = persist_tile_floats(LT);
+  constexpr int kTrig = Sw * kRow;
+  constexpr int kAp = NW * 64 * 3;
+  constexpr int nthr = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* const tiles = lds;                 // [2][kTile]
+  float* const trig = tiles + 2 * kTile;    // [2][Sw][kRow]
+  float* const apart = trig + 2 * kTrig;    // [2][NW][64][3]
+  float* const slab = apart + 2 * kAp;      // [MC4]
+  float* const Fsp = slab + MC4;            // [MC4], row-major (M, C)
+
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane / C;
+  const int c = lane - j * C;
+  const unsigned dmask = a.seg_mask[wave];
+  const int64_t P = gridDim.x;
+  const int64_t groups = a.groups;
+  const int64_t n = a.n;
+  // prologue task of this thread: task t = lane * NW + wave (spread over the waves)
+  const int t_task = lane * NW + wave;
+  const bool task = t_task < 3 * Sw;
+  const int jt = t_task / 3, q = t_task - 3 * (t_task / 3);
+  // all groups' tiles sit at the same offset mod 16 (Sw * MC * 4 = 29,040 B at l = 10)
+  const int mis = (int)(reinterpret_cast<uintptr_t>(a.gout) & 15);
+
+  auto issue_tile = [&](int64_t g, int buf) {
+    const int64_t s0 = g * Sw;
+    const int Sv = (int)min((int64_t)Sw, n - s0);
+    const int nbytes = Sv * MC * 4;
+    const char* gb = reinterpret_cast<const char*>(a.gout + s0 * MC);
+    char* stage_b = reinterpret_cast<char*>(tiles + buf * kTile) + mis;
+    const int head = min((16 - mis) & 15, nbytes);
+    const int nvec = (nbytes - head) >> 4;
+    const int tail0 = head + nvec * 16;
+    for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
+      if (v0 + lane < nvec)
+        __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(stage_b + head + 16 * v0), 16, 0, 0);
+    if (wave == NW - 1) {
+      if (4 * lane < head) __builtin_amdgcn_global_load_lds(gb + 4 * lane, as_lds(stage_b), 4, 0, 0);
+      if (tail0 + 4 * lane < nbytes)
+        __builtin_amdgcn_global_load_lds(gb + tail0 + 4 * lane, as_lds(stage_b + tail0), 4, 0, 0);
+    }
+  };
+  // the stored angle a task's slot uses (transpose: slot q takes angle 2 - q)
+  auto task_angle = [&](int64_t g) -> float {
+    const int64_t s0 = g * Sw;
+    const int Sv = (int)min((int64_t)Sw, n - s0);
+    return a.ang[(s0 + min(jt, Sv - 1)) * 3 + (a.transpose ? 2 - q : q)];
+  };
+  auto task_fill = [&](float ang, int buf) {
+    float cq, sq;
+    sincosf(ang, &sq, &cq);
+    if (a.transpose) sq = -sq;
+    trig_row_fill1<LT>(trig + buf * kTrig + jt * kRow, cq, sq, q, LT);
+  };
+
+  int64_t g = blockIdx.x;
+  // ---- first group: its tile, its multiples; the spectrum; the zeroed slab
+  float ang_next = 0.f;
+  if (task) ang_next = task_angle(g);
+  issue_tile(g, 0);
+  {
+    constexpr int kFPer = (MC + nthr - 1) / nthr;
+    float fv[kFPer];
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+      const int e = tid + nthr * k;
+      fv[k] = e < MC ? a.F[e] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+      const int e = tid + nthr * k;
+      if (e < MC) {
+        Fsp[e] = fv[k];
+        slab[e] = 0.f;
+      }
+    }
+  }
+  if (task) task_fill(ang_next, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  block_sync_lds();
+
+  const float* Fl = Fsp + c;
+  for (int k = 0; g < groups; ++k, g += P) {
+    const int cur = k & 1, nxt = cur ^ 1;
+    const int64_t gn = g + P;
+    const bool has_next = gn < groups;
+    // 1. next group's angle loads (task lanes), then its gradient tile by LDS-DMA
+    if (task && has_next) ang_next = task_angle(gn);
+    if (has_next) issue_tile(gn, nxt);
+
+    // 2. this group's chain over the wave's degrees, largest first
+    const int64_t s0 = g * Sw;
+    const int Sv = (int)min((int64_t)Sw, n - s0);
+    const bool active = j < Sv;
+    char* stage_b = reinterpret_cast<char*>(tiles + cur * kTile) + mis;
+    float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
+    const float* tj = trig + cur * kTrig + min(j, Sw - 1) * kRow;
+    float ga = 0.f, gb = 0.f, gc = 0.f;
+    sfor<LT + 1>([&](auto Lc) {
+      constexpr int l = LT - LV_CV(Lc);
+      if ((dmask >> l) & 1u) {
+        constexpr int nn = 2 * l + 1;
+        constexpr int r0 = l * l;
+        float p2[nn], p4[nn], u[nn];
+        const float* fcol = Fl + r0 * C;
+        xm_mem<l, false>(mult_lds<l, 2, LT>(tj), fcol, C, u);             // P1
+        jmul<l>(u, p2);                                                    // P2
+        xm<l>(mult_lds<l, 1, LT>(tj), p2, u);                              // P3
+        jmul<l>(u, p4);                                                    // P4
+        xm_mem<l, true>(mult_lds<l, 0, LT>(tj), tile_lane + r0 * C, C, u);  // Q4
+        ga += kdot<l>(u, p4);
+        jmul<l>(u, p4);                                                    // Q3
+        xm_t<l>(mult_lds<l, 1, LT>(tj), p4, u);                            // Q2
+        gb += kdot<l>(u, p2);
+        jmul<l>(u, p2);                                                    // Q1
+        xm_t<l>(mult_lds<l, 2, LT>(tj), p2, u);                            // dF column
+        gc += kdot_mem<l>(u, fcol, C);
+        if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
+      }
+    });
+    // 3. this wave's dF rows summed over the group's samples (sample order), added to the
+    //    block's slab (groups in the block's order)
+    wave_lds_sync();
+    {
+      const float* t0 = reinterpret_cast<const float*>(stage_b);
+      for (unsigned m = dmask; m; m &= m - 1) {
+        const int l = __builtin_ctz(m);
+        const int base = l * l * C, cnt = (2 * l + 1) * C;
+        if (Sv == Sw) {
+          constexpr int kU = 4;
+          for (int e0 = lane; e0 < cnt; e0 += kU * 64) {
+            float v[kU][Sw];
+#pragma unroll
+            for (int uu = 0; uu < kU; ++uu) {
+              const int e = base + min(e0 + 64 * uu, cnt - 1);
+#pragma unroll
+              for (int jj = 0; jj < Sw; ++jj) v[uu][jj] = t0[jj * MC + e];
+            }
+#pragma unroll
+            for (int uu = 0; uu < kU; ++uu) {
+              float sum = v[uu][0];
+#pragma unroll
+              for (int jj = 1; jj < Sw; ++jj) sum += v[uu][jj];
+              if (e0 + 64 * uu < cnt) slab[base + e0 + 64 * uu] += sum;
+            }
+          }
+        } else {
+          for (int e = lane; e < cnt; e += 64) {
+            float sum = t0[base + e];
+            for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + base + e];
+            slab[base + e] += sum;
+          }
+        }
+      }
+    }
+    // 4. the next group's multiples (its angles have long landed)
+    if (task && has_next) task_fill(ang_next, nxt);
+    // 5. angle partials; the barrier also publishes the next tile (this wave's LDS-DMA
+    //    share waited for here) and the next multiples
+    float* ap = apart + cur * kAp + wave * 64 * 3;
+    if (a.transpose) {
+      ap[lane * 3 + 0] = -gc; ap[lane * 3 + 1] = -gb; ap[lane * 3 + 2] = -ga;
+    } else {
+      ap[lane * 3 + 0] = ga; ap[lane * 3 + 1] = gb; ap[lane * 3 + 2] = gc;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    block_sync_lds();
+    // 6. the group's angle gradients: columns in order, then waves in order
+    if (tid < 3 * Sv) {
+      const int js = tid / 3, i = tid - 3 * (tid / 3);
+      const float* apc = apart + cur * kAp;
+      float r = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        float sw = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < C; ++cc) sw += apc[(w * 64 + js * C + cc) * 3 + i];
+        r += sw;
+      }
+      a.gang[(s0 + js) * 3 + i] = r;
+    }
+  }
+  // ---- the block's slab (each wave its own rows) to the workspace, chunk-major
+  for (unsigned m = dmask; m; m &= m - 1) {
+    const int l = __builtin_ctz(m);
+    const int g0 = l * l * C, cnt = (2 * l + 1) * C;
+    float* ws = a.ws_F + (int64_t)blockIdx.x * kSlabChunk;
+    const int64_t cstride = (int64_t)gridDim.x * kSlabChunk;
+    for (int e = lane; e < cnt; e += 64) {
+      const int gg = g0 + e;
+      ws[(gg / kSlabChunk) * cstride + gg % kSlabChunk] = slab[gg];
+    }
+  }
+}
+
+}  // namespace lv

@@ -372,6 +372,55 @@ def test_action_bwd_reproducible_and_looped(gpu_device):
     assert_normwise(host(f.grad)[None], gf_sum.cpu().numpy()[None], 1e-5, what="looped dF")
 
 
+def test_action_bwd_persistent_kernel(gpu_device):
+    """The persistent backward (action_bwd_persist.h: 2 blocks per CU walk the 6-sample
+    groups with the next group's gradient tile and multiples prefetched; plan mode 3 from
+    1,536 groups at l <= 10, C = 10, shared spectrum) at ragged large batches: bitwise
+    reproducible run to run; angle gradients and dF against 4,096-sample chunks (the
+    one-group kernel) at fp32 summation-order noise; the oracle's fp64 autograd on a
+    sample of the batch; transposed."""
+    import lie_vae._lib as lib
+    import lie_vae._ops as ops
+    from oracle import lie_ref
+    gen = torch.Generator().manual_seed(31)
+    L, C = 10, 10
+    M = (L + 1) ** 2
+    for n, transpose in [(9216 + 5, False), (65536, False), (30001, True)]:
+        p = lib.plan("bwd", n, L, C, 1)
+        assert p["tile"] == 3 and p["blocks"] == min(512, -(-n // 6)), p
+        ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n)).to(gpu_device)
+        F = torch.randn(M, C, generator=gen).to(gpu_device)
+        gout = torch.randn(n, M, C, generator=gen).to(gpu_device)
+        grads = []
+        for _ in range(2):
+            a = ang.clone().requires_grad_(True)
+            f = F.clone().requires_grad_(True)
+            (ops.group_action(a, f, L, transpose=transpose) * gout).sum().backward()
+            grads.append((a.grad.clone(), f.grad.clone()))
+        assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1]), \
+            ("persistent backward not reproducible", n)
+        ga_parts, gf_sum = [], torch.zeros_like(F, dtype=torch.float64)
+        for lo in range(0, n, 4096):
+            assert lib.plan("bwd", min(4096, n - lo), L, C, 1)["tile"] == 1
+            ap = ang[lo:lo + 4096].clone().requires_grad_(True)
+            fp = F.clone().requires_grad_(True)
+            (ops.group_action(ap, fp, L, transpose=transpose) * gout[lo:lo + 4096]).sum().backward()
+            ga_parts.append(ap.grad)
+            gf_sum += fp.grad.double()
+        assert_normwise(host(grads[0][0]), host(torch.cat(ga_parts)), 1e-6,
+                        what=f"persistent angle grads n={n}")
+        assert_normwise(host(grads[0][1])[None], gf_sum.cpu().numpy()[None], 1e-5,
+                        what=f"persistent dF n={n}")
+        m = 256
+        idx = torch.randperm(n, generator=gen)[:m]
+        a64 = ang[idx].cpu().double().requires_grad_(True)
+        f64 = F.cpu().double().requires_grad_(True)
+        (lie_ref.block_wigner_apply(a64, f64.expand(m, -1, -1), L, transpose=transpose)
+         * gout[idx].cpu().double()).sum().backward()
+        assert_normwise(host(grads[0][0][idx.to(gpu_device)]), a64.grad.numpy(), 1e-4,
+                        what=f"persistent gang vs oracle n={n}")
+
+
 def test_action_large_tiles_fallback_vs_oracle(gpu_device):
     """Tiles too large for the LDS plans (large C at high l; include/lievae.h plan mode 2):
     the forward's grid-stride kernel and the backward's global-spectrum fallback (dF slab
@@ -485,7 +534,7 @@ def test_fused_exp_action_bwd_matches_modular_bitwise(gpu_device):
     import lie_vae.lie_tools as lt
     torch.manual_seed(6)
     for L, C, n, transpose in [(10, 10, 4099, False), (10, 10, 777, True), (6, 3, 50000, False),
-                               (20, 16, 301, False)]:
+                               (20, 16, 301, False), (10, 10, 20003, True)]:
         M = (L + 1) ** 2
         v = torch.randn(n, 3, device=gpu_device)
         mu = lt.random_group_matrices(n, device=gpu_device).contiguous()

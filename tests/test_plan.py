@@ -10,6 +10,7 @@ LDS_PER_CU = 160 * 1024
 TILE_MAX_LDS = 80 * 1024       # action.hip kTileMaxLds
 BWD_MAX_LDS = 96 * 1024        # action.hip kBwdMaxLds
 BWD_MAX_BLOCKS = 4096          # action.hip kBwdMaxBlocks
+PERSIST_MIN_GROUPS = 1536      # action.hip kBwdPersistMinGroups
 F32, BF16 = _lib.LV_DTYPE_F32, _lib.LV_DTYPE_BF16
 NS = (1, 5, 6, 7, 683, 4096, 8192, 65536, 1 << 20)
 
@@ -67,15 +68,26 @@ def test_backward_plans_fit_the_kernels(L):
                 assert p["threads"] == 64 * p["segments"] <= 512
                 assert 3 * p["samples_per_group"] <= p["threads"]
                 assert 1 <= p["samples_per_group"] <= 64 // C
-                mode = p["tile"]  # backward: spectrum mode
-                assert mode == (0 if not shared else mode) and mode in ((1, 2) if shared else (0,))
+                mode = p["tile"]  # backward: spectrum mode (3: persistent kernel)
+                assert mode == (0 if not shared else mode) and mode in ((1, 2, 3) if shared else (0,))
+                groups = -(-n // p["samples_per_group"])
+                slab = -(-MC // 16) * 16
+                if mode == 3:
+                    # persistent kernel (action_bwd_persist.h): C = 10, l <= 10, from 1,536
+                    # groups; 2 blocks per CU, 4 waves; workspace = one slab per block + the
+                    # angle-gradient region of the fused path
+                    assert C == 10 and 3 <= L <= 10 and groups >= PERSIST_MIN_GROUPS, (L, C, n)
+                    assert p["blocks"] == min(groups, 512) and p["segments"] == 4
+                    assert 2 * p["lds_bytes"] <= LDS_PER_CU
+                    assert p["aux"] == 4 * p["blocks"] * slab + 4 * 3 * n
+                    assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
+                    continue
+                assert not (shared and C == 10 and 3 <= L <= 10 and groups >= PERSIST_MIN_GROUPS)
                 fallback = mode == 2 or p["lds_bytes"] > BWD_MAX_LDS
                 assert p["lds_bytes"] <= (LDS_PER_CU if fallback else BWD_MAX_LDS)
-                groups = -(-n // p["samples_per_group"])
                 assert p["blocks"] == min(groups, 1024 if fallback else BWD_MAX_BLOCKS)
                 # workspace: the dF slabs, one per block, sized for the chunk-major layout
                 # (16-element chunks, action_bwd.h kSlabChunk)
-                slab = -(-MC // 16) * 16
                 assert p["aux"] == (4 * p["blocks"] * slab if shared else 0)
                 assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
 
