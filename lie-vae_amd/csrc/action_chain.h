@@ -110,28 +110,41 @@ __device__ __forceinline__ void trig_row_fill(float* tj, const float c1[3], cons
   });
 }
 
-// The same for one slot whose (cos, sin) the caller already picked (bitwise equal).
+// The same for one slot whose (cos, sin) the caller already picked (bitwise equal).  The
+// row is written with 16-byte LDS stores once the recurrence is done (entries past `upto`
+// and up to TP - 1 are zero): 2 * TP / 4 stores instead of 2 * (upto + 1) scalar ones on
+// the prologue's critical path.
 template <int LT>
 __device__ __forceinline__ void trig_row_fill1(float* tj, float cq, float sq, int q, int upto) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int TP = TrigLds<LT>::TP;
-  float* tc = tj + 2 * q * TP;
-  float* ts = tc + TP;
-  tc[0] = 1.f;
-  ts[0] = 0.f;
+  float cv[TP], sv[TP];
+  cv[0] = 1.f;
+  sv[0] = 0.f;
   float cf = cq, sf = sq;
-  sfor<LT + 1>([&](auto F) {
+  sfor<TP>([&](auto F) {
     constexpr int f = LV_CV(F);
     if constexpr (f >= 1) {
-      if (f <= upto) {
+      if (f <= LT && f <= upto) {
         if constexpr (f >= 2) {
           const float cn = fmaf(cf, cq, -(sf * sq));
           sf = fmaf(sf, cq, cf * sq);
           cf = cn;
         }
-        tc[f] = cf;
-        ts[f] = sf;
+        cv[f] = cf;
+        sv[f] = sf;
+      } else {
+        cv[f] = 0.f;
+        sv[f] = 0.f;
       }
     }
+  });
+  f4* tc = reinterpret_cast<f4*>(tj + 2 * q * TP);
+  f4* ts = reinterpret_cast<f4*>(tj + (2 * q + 1) * TP);
+  sfor<TP / 4>([&](auto K) {
+    constexpr int k = LV_CV(K);
+    tc[k] = f4{cv[4 * k], cv[4 * k + 1], cv[4 * k + 2], cv[4 * k + 3]};
+    ts[k] = f4{sv[4 * k], sv[4 * k + 1], sv[4 * k + 2], sv[4 * k + 3]};
   });
 }
 

@@ -310,6 +310,17 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
   LaneIn in;
   if (task) lane_load<FUSED, MAYMU>(a, st, in);
+  // the mu-free fused kernel writes ang_out (the product operator's saved angles) from the
+  // LAST wave, lanes j < Sv, after that wave's chain: off the prologue's critical path
+  // (quat_to_eazyz_fwd's atan2 / acos on the q = 0 task lanes held wave 0's multiples by
+  // ~0.5 us per launch).  Same quaternion (exp_quat), so the same angles bit for bit.
+  constexpr bool kAngLate = FUSED && !MAYMU;
+  const bool ang_lane = kAngLate && a.ang_out != nullptr && wave == (nthr >> 6) - 1 && lane < Sv;
+  float vang[3] = {0.f, 0.f, 0.f};
+  if (ang_lane) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vang[i] = a.v[(s0 + lane) * 3 + i];
+  }
   // 2. spectrum staging: every load issued now (before the prologue maths), the LDS writes
   //    after it.  CT > 0: element e = tid + k * nthr of the whole (M, C) spectrum, at most
   //    kFPer per thread for the smallest block the plan makes (2 waves), a batched loop
@@ -334,16 +345,11 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     float cq, sq;
     if constexpr (FUSED && !MAYMU) {
       // z = exp(v): this thread's slot only (transpose: slot q takes angle 2 - q, sine negated)
+      // ang_out is written after the chain by the last wave (below): its atan2 / acos
+      // chain kept the multiples waiting on the q = 0 lanes
       float qr[4];
       exp_to_zyz_slot(in.v, a.transpose ? 2 - q : q, cq, sq, qr);
       if (a.transpose) sq = -sq;
-      if (a.ang_out && jt < Sv && q == 0) {
-        float ang[3];
-        quat_to_eazyz_fwd(qr, ang);
-        a.ang_out[st * 3 + 0] = ang[0];
-        a.ang_out[st * 3 + 1] = ang[1];
-        a.ang_out[st * 3 + 2] = ang[2];
-      }
     } else {
       float c1[3], s1[3];
       lane_angles<FUSED, MAYMU>(a, in, st, jt < Sv, q, FUSED && a.ang_out != nullptr, c1, s1);
@@ -415,6 +421,14 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
       if (a.stamps) degree_stamp(a.stamps, wave, l);
     }
   });
+  if (ang_lane) {
+    const ExpQuat e = exp_quat(vang);
+    float ang[3];
+    quat_to_eazyz_fwd(e.qr, ang);
+    a.ang_out[(s0 + lane) * 3 + 0] = ang[0];
+    a.ang_out[(s0 + lane) * 3 + 1] = ang[1];
+    a.ang_out[(s0 + lane) * 3 + 2] = ang[2];
+  }
   phase_stamp(a.stamps, wave, 2);
   block_sync_lds();
   phase_stamp(a.stamps, wave, 3);
