@@ -372,6 +372,8 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   a.write_through = (int64_t)a.n * a.MC * out_bytes <= kWriteThroughMaxBytes ? 1 : 0;
   if (kEnvWT >= 0) a.write_through = kEnvWT;
   a.prio = kEnvPrio;
+  static const int kEnvSpread = LV_KNOB("LV_TILE_SPREAD", 0);  // A/B: prologue tasks over all waves
+  a.task_spread = kEnvSpread;
   p.tile = true;
   p.lds = lds;
   p.gx = (int)groups;

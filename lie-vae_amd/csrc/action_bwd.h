@@ -39,6 +39,8 @@ constexpr int kBwdVarSlabFlat = 2, kBwdVarSlabWT = 4;
 // wave's first (largest) degree computes its forward recompute P1..P4 -- which needs the
 // multiples and the spectrum, not the gradient tile -- while the tile's LDS-DMA is in flight
 constexpr int kBwdVarSplit = 8;
+// prologue tasks spread over the block's waves (see action_bwd_tile_kernel)
+constexpr int kBwdVarSpread = 16;
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
@@ -265,8 +267,11 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
   // and may split the prologue barrier (kBwdVarSplit: the largest degree's forward
   // recompute overlapping the tile DMA)
   constexpr bool kDesc = CT > 0 && !LOOP && FM == kBwdFShared;
-  const bool task = tid < 3 * Sw;  // the host guarantees 3*Sw <= blockDim.x
-  const int jt = tid / 3, q = tid - 3 * (tid / 3);
+  // kBwdVarSpread: task t on lane t / nw of wave t % nw (the prologue's serial chains on
+  // every SIMD), else thread t (all tasks in wave 0); the host guarantees 3*Sw <= blockDim.x
+  const int t_task = (a.variant & kBwdVarSpread) ? lane * (nthr >> 6) + wave : tid;
+  const bool task = t_task < 3 * Sw;
+  const int jt = t_task / 3, q = t_task - 3 * (t_task / 3);
   // kDesc: the prologue's angle and the VJP tail's v / mu loaded before the spectrum, so
   // the spectrum staging's wait covers them and nothing after the tile DMA waits in vmcnt
   // order behind it

@@ -28,6 +28,8 @@ struct ActionArgs {
   int write_through;    // tile kernel: 1 = sc1 (write-through) stores, 0 = nt stores, 2 = plain (A/B)
   int prio;             // tile kernel wave priority: 2 = prologue at s_setprio 3, chain at 0
                         // (default); A/B: 0 off, 1 flush at 3, 3 = 2 + flush at 2
+  int task_spread;      // tile kernel: prologue task t on lane t / nw of wave t % nw (1) instead
+                        // of thread t (0: all tasks in wave 0)
   unsigned long long* stamps;  // phase timestamps (A/B timeline tool; null in the product)
   int seg_lo[kMaxSeg + 1];      // non-tile kernel / run-time-C tile: contiguous degree ranges
   unsigned seg_mask[kMaxSeg];   // tile kernel: degree set of wave k (bit l = degree l)

@@ -305,8 +305,11 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   // starts at once, unchanged).  1 / 3: A/B variants with the flush raised.
   phase_stamp(a.stamps, wave, 0);
   if (a.prio >= 2) __builtin_amdgcn_s_setprio(3);
-  const bool task = tid < 3 * Sw;
-  const int jt = tid / 3, q = tid - 3 * (tid / 3);
+  // task_spread: task t on lane t / nw of wave t % nw, so the prologue's serial chains run on
+  // every SIMD of the CU instead of all in wave 0
+  const int t_task = a.task_spread ? lane * (nthr >> 6) + wave : tid;
+  const bool task = t_task < 3 * Sw;
+  const int jt = t_task / 3, q = t_task - 3 * (t_task / 3);
   const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
   LaneIn in;
   if (task) lane_load<FUSED, MAYMU>(a, st, in);

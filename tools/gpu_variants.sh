@@ -15,7 +15,7 @@ for spec in "$@"; do
   IFS=',' read -ra kv <<< "$envs"
   timeout -k 10 120 env ${kv[@]+"${kv[@]}"} python tools/c5_hash.py > $OUT/$tag.hash 2>&1 || { echo "$tag hash failed"; tail -3 $OUT/$tag.hash; exit 1; }
   timeout -k 10 300 env ${kv[@]+"${kv[@]}"} python bench.py $BARGS --steps 400 --warmup 40 --no-fwd-bwd --no-cpu-baseline \
-      --cold-launches 0 --multistream 1 > $OUT/$tag.log 2>&1 || { echo "$tag bench failed"; tail -3 $OUT/$tag.log; exit 1; }
+      --cold-launches 0 --multistream 1 --config5-launches 0 --train-steps 0 > $OUT/$tag.log 2>&1 || { echo "$tag bench failed"; tail -3 $OUT/$tag.log; exit 1; }
   python3 - "$tag" $OUT/$tag.log $OUT/$tag.hash <<'PY'
 import json, sys
 d = [json.loads(l) for l in open(sys.argv[2]) if l.startswith("{")][-1]
