@@ -407,7 +407,7 @@ def test_action_bwd_persistent_kernel(gpu_device):
             (ops.group_action(ap, fp, L, transpose=transpose) * gout[lo:lo + 4096]).sum().backward()
             ga_parts.append(ap.grad)
             gf_sum += fp.grad.double()
-        assert_normwise(host(grads[0][0]), host(torch.cat(ga_parts)), 1e-6,
+        assert_normwise(host(grads[0][0]), host(torch.cat(ga_parts)), 1e-5,
                         what=f"persistent angle grads n={n}")
         assert_normwise(host(grads[0][1])[None], gf_sum.cpu().numpy()[None], 1e-5,
                         what=f"persistent dF n={n}")
