@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=10,
                     help="train_step record: timed steps per precision (0: skip the record)")
     ap.add_argument("--train-warmup", type=int, default=3)
+    ap.add_argument("--no-ang", action="store_true",
+                    help="A/B only: time the instantiation without the angles output")
     ap.add_argument("--dry-run", action="store_true",
                     help="rehearse the rank plumbing on CPU (gloo, no HIP call)")
     return ap.parse_args()
@@ -212,8 +214,8 @@ def main():
         o = out if o is None else o
         vv = v if vv is None else vv
         a = ang_buf if a is None else a
-        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(vv), P(F), 0, P(o), dt, P(a), nb, L, C,
-                                                0, k, s)
+        rc = lib.lv_fused_exp_action_fwd_repeat(None, P(vv), P(F), 0, P(o), dt,
+                                                None if args.no_ang else P(a), nb, L, C, 0, k, s)
         if rc:
             raise RuntimeError(_lib.last_error())
 
@@ -489,8 +491,9 @@ def main():
                                             "submission cost both brackets hold cancels. The "
                                             "raw t_K / K is us_per_launch_events_raw",
                          "events": "graph nodes" if events_in_graph else "stream",
-                         "instantiation": "product (angles written, as torch.ops.lievae."
-                                          "fused_exp_action)",
+                         "instantiation": ("A/B: no angles output" if args.no_ang else
+                                           "product (angles written, as torch.ops.lievae."
+                                           "fused_exp_action)"),
                          "cache": "hot (back-to-back launches)"},
             "cache_cold": cache_cold,
             "cpu_baseline": cpu,

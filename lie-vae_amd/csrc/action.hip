@@ -551,7 +551,7 @@ struct BwdPlan {
 // per CU walk the groups with the next group's gradient tile and multiples prefetched under
 // the current chain, one dF slab per block.  Below it the one-group kernel's single round
 // of blocks is shorter.
-constexpr int64_t kBwdPersistMinGroups = 1536;
+constexpr int64_t kBwdPersistMinGroups = 4097;
 
 bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   static const int kEnvNseg = LV_KNOB("LV_BWD_NSEG", 0);      // A/B testing only

@@ -313,17 +313,27 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
   const int64_t st = s0 + min(jt, Sv - 1);  // idle slots mirror a valid sample
   LaneIn in;
   if (task) lane_load<FUSED, MAYMU>(a, st, in);
-  // the mu-free fused kernel writes ang_out (the product operator's saved angles) from the
-  // LAST wave, lanes j < Sv, after that wave's chain: off the prologue's critical path
-  // (quat_to_eazyz_fwd's atan2 / acos on the q = 0 task lanes held wave 0's multiples by
-  // ~0.5 us per launch).  Same quaternion (exp_quat), so the same angles bit for bit.
+  // The mu-free fused kernel writes ang_out (the product operator's saved angles) from
+  // wave 1, lanes j < Sv, during the prologue -- a wave that only stages spectrum rows
+  // there, on another SIMD than the task lanes of wave 0 -- instead of on the q = 0 task
+  // lanes, where quat_to_eazyz_fwd's atan2 / acos held wave 0's multiples by ~0.5 us per
+  // launch.  Same quaternion (exp_quat), so the same angles bit for bit.  (A one-wave
+  // block writes them after its chain.)
   constexpr bool kAngLate = FUSED && !MAYMU;
-  const bool ang_lane = kAngLate && a.ang_out != nullptr && wave == (nthr >> 6) - 1 && lane < Sv;
-  float vang[3] = {0.f, 0.f, 0.f};
-  if (ang_lane) {
+  const int ang_wave = (nthr >> 6) > 1 ? 1 : 0;
+  const bool ang_lane = kAngLate && a.ang_out != nullptr && wave == ang_wave && lane < Sv;
+  auto write_ang = [&]() {
+    float vang[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) vang[i] = a.v[(s0 + lane) * 3 + i];
-  }
+    const ExpQuat e = exp_quat(vang);
+    float ang[3];
+    quat_to_eazyz_fwd(e.qr, ang);
+    a.ang_out[(s0 + lane) * 3 + 0] = ang[0];
+    a.ang_out[(s0 + lane) * 3 + 1] = ang[1];
+    a.ang_out[(s0 + lane) * 3 + 2] = ang[2];
+  };
+  if (ang_lane && ang_wave == 1) write_ang();
   // 2. spectrum staging: every load issued now (before the prologue maths), the LDS writes
   //    after it.  CT > 0: element e = tid + k * nthr of the whole (M, C) spectrum, at most
   //    kFPer per thread for the smallest block the plan makes (2 waves), a batched loop
@@ -424,14 +434,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
       if (a.stamps) degree_stamp(a.stamps, wave, l);
     }
   });
-  if (ang_lane) {
-    const ExpQuat e = exp_quat(vang);
-    float ang[3];
-    quat_to_eazyz_fwd(e.qr, ang);
-    a.ang_out[(s0 + lane) * 3 + 0] = ang[0];
-    a.ang_out[(s0 + lane) * 3 + 1] = ang[1];
-    a.ang_out[(s0 + lane) * 3 + 2] = ang[2];
-  }
+  if (ang_lane && ang_wave == 0) write_ang();
   phase_stamp(a.stamps, wave, 2);
   block_sync_lds();
   phase_stamp(a.stamps, wave, 3);
