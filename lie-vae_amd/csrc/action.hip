@@ -569,10 +569,12 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       b.nseg = kBwdPersistWaves;
       b.fmode = kBwdFShared;
       b.groups = groups;
-      b.gx = (int)std::min<int64_t>(groups, kBwdCUs * kBwdPersistBlocksPerCU);
+      static const int kEnvVariantP = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
+      const bool single = (kEnvVariantP & kBwdVarPersistSingle) != 0;  // A/B: one tile buffer
+      b.gx = (int)std::min<int64_t>(groups, kBwdCUs * (single ? 3 : kBwdPersistBlocksPerCU));
       plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
       balance_masks(L, b.nseg, true, b.seg_mask);
-      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, kBwdPersistWaves);
+      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, kBwdPersistWaves, single ? 1 : 2);
       const size_t slabs = sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk);
       b.ws_gang_off = slabs;
       b.ws = slabs + sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);

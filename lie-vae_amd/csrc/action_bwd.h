@@ -633,8 +633,18 @@ template <int LT>
 int BwdLauncher<LT>::run(BwdLaunch& p) {
   const dim3 grid(p.gx), block(64 * p.nseg);
   if (p.persist) {
-    if constexpr (LT <= kBwdPersistMaxL)
-      hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves>), grid, block, p.lds, p.stream, p.a);
+    if constexpr (LT <= kBwdPersistMaxL) {
+      const bool single = (p.a.variant & kBwdVarPersistSingle) != 0;
+      const bool nojit = (p.a.variant & kBwdVarPersistNoJit) != 0;
+      if (single && nojit)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, false>), grid, block, p.lds, p.stream, p.a);
+      else if (single)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true>), grid, block, p.lds, p.stream, p.a);
+      else if (nojit)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, true, false>), grid, block, p.lds, p.stream, p.a);
+      else
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves>), grid, block, p.lds, p.stream, p.a);
+    }
     LV_RETURN_LAUNCH("action_bwd_persist_kernel");
   }
   if (p.fmode == kBwdFSample)

@@ -33,19 +33,26 @@ namespace lv {
 constexpr int kBwdPersistMaxL = 10;
 constexpr int kBwdPersistWaves = 4;      // degree-set waves per block
 constexpr int kBwdPersistBlocksPerCU = 2;
+// A/B variant bits of the persistent kernel (ActionBwdArgs::variant, A/B build only):
+// single gradient-tile buffer at 3 blocks per CU (3 waves per SIMD; the next tile is
+// loaded after the group's barrier), and the non-JIT chain (spectrum / gradient columns
+// read into registers at each product)
+constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistNoJit = 64;
 
-// LDS floats of the persistent kernel: 2 tiles, 2 multiples tables, 2 angle-partial
-// buffers, the dF slab and the spectrum.
+// LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
+// multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
 __host__ __device__ constexpr int persist_tile_floats(int L) {
   return (((64 / 10) * (L + 1) * (L + 1) * 10 * 4 + 16 + 15) & ~15) / 4;
 }
-__host__ __device__ constexpr int persist_lds_floats(int L, int NW) {
-  return 2 * persist_tile_floats(L) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
+__host__ __device__ constexpr int persist_lds_floats(int L, int NW, int NB = 2) {
+  return NB * persist_tile_floats(L) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
          2 * ((((L + 1) * (L + 1) * 10) + 3) & ~3);
 }
 
-template <int LT, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
+// DB: double-buffered gradient tile (2 blocks per CU); else one buffer at 3 blocks per CU.
+// JIT: spectrum / gradient columns read in row pairs inside the products.
+template <int LT, int NW, bool DB = true, bool JIT = true>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DB ? 2 : 3)))
 void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr int C = kTileFastC;
   constexpr int Sw = 64 / C;
@@ -56,9 +63,10 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr int kTrig = Sw * kRow;
   constexpr int kAp = NW * 64 * 3;
   constexpr int nthr = 64 * NW;
+  constexpr int NB = DB ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* const tiles = lds;                 // [2][kTile]
-  float* const trig = tiles + 2 * kTile;    // [2][Sw][kRow]
+  float* const tiles = lds;                 // [NB][kTile]
+  float* const trig = tiles + NB * kTile;   // [2][Sw][kRow]
   float* const apart = trig + 2 * kTrig;    // [2][NW][64][3]
   float* const slab = apart + 2 * kAp;      // [MC4]
   float* const Fsp = slab + MC4;            // [MC4], row-major (M, C)
@@ -139,17 +147,19 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   const float* Fl = Fsp + c;
   for (int k = 0; g < groups; ++k, g += P) {
     const int cur = k & 1, nxt = cur ^ 1;
+    const int tcur = DB ? cur : 0;
     const int64_t gn = g + P;
     const bool has_next = gn < groups;
-    // 1. next group's angle loads (task lanes), then its gradient tile by LDS-DMA
+    // 1. next group's angle loads (task lanes), then (double buffer) its gradient tile by
+    //    LDS-DMA; a single buffer is refilled after this group's barrier (step 7)
     if (task && has_next) ang_next = task_angle(gn);
-    if (has_next) issue_tile(gn, nxt);
+    if (DB && has_next) issue_tile(gn, nxt);
 
     // 2. this group's chain over the wave's degrees, largest first
     const int64_t s0 = g * Sw;
     const int Sv = (int)min((int64_t)Sw, n - s0);
     const bool active = j < Sv;
-    char* stage_b = reinterpret_cast<char*>(tiles + cur * kTile) + mis;
+    char* stage_b = reinterpret_cast<char*>(tiles + tcur * kTile) + mis;
     float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
     const float* tj = trig + cur * kTrig + min(j, Sw - 1) * kRow;
     float ga = 0.f, gb = 0.f, gc = 0.f;
@@ -160,18 +170,36 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         constexpr int r0 = l * l;
         float p2[nn], p4[nn], u[nn];
         const float* fcol = Fl + r0 * C;
-        xm_mem<l, false>(mult_lds<l, 2, LT>(tj), fcol, C, u);             // P1
+        if constexpr (JIT) {
+          xm_mem<l, false>(mult_lds<l, 2, LT>(tj), fcol, C, u);           // P1
+        } else {
+          float f0[nn];
+          sfor<nn>([&](auto K) { f0[LV_CV(K)] = fcol[LV_CV(K) * C]; });
+          xm<l>(mult_lds<l, 2, LT>(tj), f0, u);
+        }
         jmul<l>(u, p2);                                                    // P2
         xm<l>(mult_lds<l, 1, LT>(tj), p2, u);                              // P3
         jmul<l>(u, p4);                                                    // P4
-        xm_mem<l, true>(mult_lds<l, 0, LT>(tj), tile_lane + r0 * C, C, u);  // Q4
+        if constexpr (JIT) {
+          xm_mem<l, true>(mult_lds<l, 0, LT>(tj), tile_lane + r0 * C, C, u);  // Q4
+        } else {
+          float gq[nn];
+          sfor<nn>([&](auto K) { gq[LV_CV(K)] = tile_lane[(r0 + LV_CV(K)) * C]; });
+          xm_t<l>(mult_lds<l, 0, LT>(tj), gq, u);
+        }
         ga += kdot<l>(u, p4);
         jmul<l>(u, p4);                                                    // Q3
         xm_t<l>(mult_lds<l, 1, LT>(tj), p4, u);                            // Q2
         gb += kdot<l>(u, p2);
         jmul<l>(u, p2);                                                    // Q1
         xm_t<l>(mult_lds<l, 2, LT>(tj), p2, u);                            // dF column
-        gc += kdot_mem<l>(u, fcol, C);
+        if constexpr (JIT) {
+          gc += kdot_mem<l>(u, fcol, C);
+        } else {
+          float f0[nn];
+          sfor<nn>([&](auto K) { f0[LV_CV(K)] = fcol[LV_CV(K) * C]; });
+          gc += kdot<l>(u, f0);
+        }
         if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
       }
     });
@@ -222,9 +250,11 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     block_sync_lds();
-    // 6. the group's angle gradients: columns in order, then waves in order
-    if (tid < 3 * Sv) {
-      const int js = tid / 3, i = tid - 3 * (tid / 3);
+    // 6. the group's angle gradients (columns in order, then waves in order), output t on
+    //    lane t / NW of wave t % NW: no wave carries all 18 serial 40-term sums into its
+    //    next chain
+    if (t_task < 3 * Sv) {
+      const int js = t_task / 3, i = t_task - 3 * (t_task / 3);
       const float* apc = apart + cur * kAp;
       float r = 0.f;
 #pragma unroll
@@ -235,6 +265,15 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         r += sw;
       }
       a.gang[(s0 + js) * 3 + i] = r;
+    }
+    // 7. single buffer: every wave is past this group's chain and slab pass (the barrier
+    //    above), so the tile takes the next group now; its wait and barrier follow
+    if constexpr (!DB) {
+      if (has_next) {
+        issue_tile(gn, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        block_sync_lds();
+      }
     }
   }
   // ---- the block's slab (each wave its own rows) to the workspace, chunk-major

@@ -220,6 +220,9 @@ __device__ __forceinline__ float xrot_dot_deriv(const TrigTab<LT>& t, const floa
 }
 
 // y = J_l x with J_l's non-zeros as literal coefficients (J is symmetric: J^T = J).
+#ifndef LV_JMUL_MUL
+#define LV_JMUL_MUL 1
+#endif
 template <int l>
 __device__ __forceinline__ void jmul(const float (&x)[2 * l + 1], float (&y)[2 * l + 1]) {
   constexpr int n = 2 * l + 1;
@@ -227,10 +230,18 @@ __device__ __forceinline__ void jmul(const float (&x)[2 * l + 1], float (&y)[2 *
   sfor<n>([&](auto P) {
     constexpr int p = LV_CV(P);
     float acc = 0.f;
+    bool first = true;
     sfor<n>([&](auto K) {
       constexpr int k = LV_CV(K);
       constexpr float v = J[p * n + k];
-      if constexpr (v != 0.f) acc = fmaf(v, x[k], acc);
+      if constexpr (v != 0.f) {
+        // LV_JMUL_MUL: the row's first term as a multiply (v_mul_f32 takes the literal;
+        // fma(v, x, 0) needs it in an SGPR, one s_mov per row) -- equal except for the
+        // sign of an all-zero row's result
+        if (LV_JMUL_MUL && first) acc = v * x[k];
+        else acc = fmaf(v, x[k], acc);
+        first = false;
+      }
     });
     y[p] = acc;
   });
