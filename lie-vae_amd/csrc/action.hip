@@ -571,10 +571,11 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       b.groups = groups;
       static const int kEnvVariantP = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
       const bool single = (kEnvVariantP & kBwdVarPersistSingle) != 0;  // A/B: one tile buffer
+      if (kEnvVariantP & kBwdVarPersistNW5) b.nseg = 5;                 // A/B: 5 waves per block
       b.gx = (int)std::min<int64_t>(groups, kBwdCUs * (single ? 3 : kBwdPersistBlocksPerCU));
       plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
       balance_masks(L, b.nseg, true, b.seg_mask);
-      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, kBwdPersistWaves, single ? 1 : 2);
+      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, b.nseg, single ? 1 : 2);
       const size_t slabs = sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk);
       b.ws_gang_off = slabs;
       b.ws = slabs + sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);

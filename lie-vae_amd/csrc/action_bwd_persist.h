@@ -38,6 +38,9 @@ constexpr int kBwdPersistBlocksPerCU = 2;
 // loaded after the group's barrier), and the non-JIT chain (spectrum / gradient columns
 // read into registers at each product)
 constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistNoJit = 64;
+// ... and 5 degree-set waves per block (10 per CU: the l = 10 set is then ~1.1x the mean
+// per-wave chain instead of ~0.85x of a 4-way split), built for 3 waves per SIMD
+constexpr int kBwdVarPersistNW5 = 128;
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
@@ -51,8 +54,8 @@ __host__ __device__ constexpr int persist_lds_floats(int L, int NW, int NB = 2) 
 
 // DB: double-buffered gradient tile (2 blocks per CU); else one buffer at 3 blocks per CU.
 // JIT: spectrum / gradient columns read in row pairs inside the products.
-template <int LT, int NW, bool DB = true, bool JIT = true>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DB ? 2 : 3)))
+template <int LT, int NW, bool DB = true, bool JIT = true, int WPE = (DB ? 2 : 3)>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE)))
 void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr int C = kTileFastC;
   constexpr int Sw = 64 / C;
