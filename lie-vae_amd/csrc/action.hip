@@ -528,7 +528,10 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 constexpr int64_t kBwdCUs = 256;  // MI355X compute units
 constexpr int kBwdReduceDefault = 3;  // LV_BWD_REDUCE default (see action_bwd_common)
-constexpr int kBwdVariantDefault = kBwdVarJit;  // LV_BWD_VARIANT default (kBwdVar* bits; profiles/r04_bwd_reduce_ab.txt)
+// LV_BWD_VARIANT default (kBwdVar* bits): JIT chain (profiles/r04_bwd_reduce_ab.txt); the
+// persistent kernel with one tile buffer at 3 blocks per CU (65,536: 131 -> 114 us against
+// the double-buffered 2 blocks per CU, profiles/r05_ab4.txt)
+constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle;
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in

@@ -9,17 +9,18 @@
 // third of the gradient tile's bytes again at l = 10, read back by the reduce).  Beyond
 // 4,096 groups the grid was capped and blocks looped over groups in a 256-VGPR build.
 //
-// Here a grid of 2 blocks per CU walks the groups (block b: groups b, b + P, b + 2P, ...),
-// and each block overlaps group k's chain with group k+1's loads:
-//   * the gradient tile of group k+1 goes global -> LDS by LDS-DMA into the second of two
-//     tile buffers while the waves run group k's chain (no VGPR holds it in flight);
+// Here a grid of 3 blocks per CU walks the groups (block b: groups b, b + P, b + 2P, ...):
 //   * the prologue of group k+1 (sincos of the stored angle, multiples of one (sample,
 //     slot) per task lane, tasks spread over the block's waves) runs after each wave's
 //     chain, into the second of two multiples tables, its angle loads issued at the top;
 //   * each wave adds its degrees' dF rows, summed over the group's samples, into the
 //     block's LDS slab (its own rows only: no race); the slab leaves once per block;
-//   * ONE block barrier per group: it publishes the angle partials, the next tile and the
-//     next multiples, and frees the current buffers.
+//   * one barrier per group publishes the angle partials and the next multiples and
+//     frees the gradient tile, which then takes the next group by LDS-DMA (no VGPR holds
+//     it in flight) before a second barrier.
+// DB = true double-buffers the gradient tile instead (the next tile's DMA under the current
+// chain, one barrier per group) at 2 blocks per CU; measured slower than 3 blocks per CU
+// with one buffer (65,536: 131 vs 114 us, profiles/r05_ab4.txt), kept as A/B variant.
 // The chain itself (P1..P4 forward recompute, Q4..dF transposed chain, angle gradients as
 // <Q4, K P4>, <Q2, K P2>, <dF, K F>) is the one-group kernel's JIT chain, operation for
 // operation.  Summation orders are fixed by the plan (degree set per wave, groups per

@@ -74,11 +74,11 @@ def test_backward_plans_fit_the_kernels(L):
                 slab = -(-MC // 16) * 16
                 if mode == 3:
                     # persistent kernel (action_bwd_persist.h): C = 10, l <= 10, from 4,097
-                    # groups; 2 blocks per CU, 4 waves; workspace = one slab per block + the
-                    # angle-gradient region of the fused path
+                    # groups; one gradient-tile buffer, 3 blocks per CU, 4 waves; workspace =
+                    # one slab per block + the angle-gradient region of the fused path
                     assert C == 10 and 3 <= L <= 10 and groups >= PERSIST_MIN_GROUPS, (L, C, n)
-                    assert p["blocks"] == min(groups, 512) and p["segments"] == 4
-                    assert 2 * p["lds_bytes"] <= LDS_PER_CU
+                    assert p["blocks"] == min(groups, 768) and p["segments"] == 4
+                    assert 3 * p["lds_bytes"] <= LDS_PER_CU
                     assert p["aux"] == 4 * p["blocks"] * slab + 4 * 3 * n
                     assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
                     continue
