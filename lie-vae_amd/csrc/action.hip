@@ -550,11 +550,13 @@ struct BwdPlan {
   size_t lds, ws;
 };
 
-// Persistent backward (action_bwd_persist.h) from this many 6-sample groups up: 2 blocks
-// per CU walk the groups with the next group's gradient tile and multiples prefetched under
-// the current chain, one dF slab per block.  Below it the one-group kernel's single round
-// of blocks is shorter.
-constexpr int64_t kBwdPersistMinGroups = 4097;
+// Persistent backward (action_bwd_persist.h) from this many 6-sample groups up, i.e. once
+// the batch needs more than one round of 3 blocks per CU: 3 blocks per CU walk the groups,
+// the next group's multiples prefetched, one dF slab per block.  Below it the one-group
+// kernel (one round of blocks, the fused VJP in its tail) is shorter (4,096: 14.26 vs
+// 14.47 us; 9,216: 24.9 vs 23.1; 16,384: 38.8 vs 33.5; 65,536: 182 vs 110,
+// profiles/r05_bwd_persist_ab2.txt).
+constexpr int64_t kBwdPersistMinGroups = 769;
 
 bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   static const int kEnvNseg = LV_KNOB("LV_BWD_NSEG", 0);      // A/B testing only

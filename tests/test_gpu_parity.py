@@ -375,7 +375,7 @@ def test_action_bwd_reproducible_and_looped(gpu_device):
 def test_action_bwd_persistent_kernel(gpu_device):
     """The persistent backward (action_bwd_persist.h: 3 blocks per CU walk the 6-sample
     groups, the next group's multiples prefetched, one dF slab per block; plan mode 3 from
-    4,097 groups at l <= 10, C = 10, shared spectrum) at ragged large batches: bitwise
+    769 groups at l <= 10, C = 10, shared spectrum) at ragged large batches: bitwise
     reproducible run to run; angle gradients and dF against 4,096-sample chunks (the
     one-group kernel) at fp32 summation-order noise; the oracle's fp64 autograd on a
     sample of the batch; transposed."""
@@ -385,7 +385,7 @@ def test_action_bwd_persistent_kernel(gpu_device):
     gen = torch.Generator().manual_seed(31)
     L, C = 10, 10
     M = (L + 1) ** 2
-    for n, transpose in [(6 * 4097 + 5, False), (65536, False), (30001, True)]:
+    for n, transpose in [(6 * 769 + 5, False), (65536, False), (30001, True)]:
         p = lib.plan("bwd", n, L, C, 1)
         assert p["tile"] == 3 and p["blocks"] == min(768, -(-n // 6)), p
         ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n)).to(gpu_device)

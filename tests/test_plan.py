@@ -10,7 +10,7 @@ LDS_PER_CU = 160 * 1024
 TILE_MAX_LDS = 80 * 1024       # action.hip kTileMaxLds
 BWD_MAX_LDS = 96 * 1024        # action.hip kBwdMaxLds
 BWD_MAX_BLOCKS = 4096          # action.hip kBwdMaxBlocks
-PERSIST_MIN_GROUPS = 4097      # action.hip kBwdPersistMinGroups
+PERSIST_MIN_GROUPS = 769       # action.hip kBwdPersistMinGroups
 F32, BF16 = _lib.LV_DTYPE_F32, _lib.LV_DTYPE_BF16
 NS = (1, 5, 6, 7, 683, 4096, 8192, 65536, 1 << 20)
 
@@ -73,7 +73,7 @@ def test_backward_plans_fit_the_kernels(L):
                 groups = -(-n // p["samples_per_group"])
                 slab = -(-MC // 16) * 16
                 if mode == 3:
-                    # persistent kernel (action_bwd_persist.h): C = 10, l <= 10, from 4,097
+                    # persistent kernel (action_bwd_persist.h): C = 10, l <= 10, from 769
                     # groups; one gradient-tile buffer, 3 blocks per CU, 4 waves; workspace =
                     # one slab per block + the angle-gradient region of the fused path
                     assert C == 10 and 3 <= L <= 10 and groups >= PERSIST_MIN_GROUPS, (L, C, n)
