@@ -662,10 +662,17 @@ def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     torch.cuda.synchronize(dev)
     tg = e0.elapsed_time(e1) / 1e3 / reps
     kern = bench_action_bwd_kernel(vg.detach(), F, gout, L, dev)
+    # the large-batch backward (persistent kernel, action_bwd_persist.h) at 65,536 samples
+    g2 = torch.Generator(device="cpu").manual_seed(77)
+    vb = torch.randn(65536, 3, generator=g2).to(dev)
+    gb = torch.randn(65536, (L + 1) ** 2, C, generator=g2).to(dev)
+    kern_big = bench_action_bwd_kernel(vb, F, gb, L, dev, reps=100)
+    del vb, gb
     return {"value": B / tg, "unit": "samples/s", "us_per_step": tg * 1e6,
             "launch": "graph (forward + backward captured once, replayed)",
             "eager_us_per_step": t * 1e6, "eager_value": B / t,
             "action_bwd": kern,
+            "action_bwd_65536": kern_big,
             "note": "one training-direction pass: fused forward, group-action backward "
                     "kernel + deterministic dF reduce + fused exp/ZYZ VJP"}
 
@@ -714,11 +721,19 @@ def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):
     e1.record(cur)
     torch.cuda.synchronize(dev)
     us = e0.elapsed_time(e1) * 1e3 / (reps // 50 * 50)
-    bb = B * (12 + M * C * 4 + 12) + 2 * M * C * 4 + ws_bytes * 2
-    return {"us_per_call": us, "samples_per_s": B / us * 1e6, "bytes_per_call": bb,
+    plan = _lib.plan("bwd", B, L, C, 1)
+    slab_bytes = plan["blocks"] * (-(-M * C // 16) * 16) * 4
+    bb = B * (12 + M * C * 4 + 12) + 2 * M * C * 4 + slab_bytes * 2
+    bmin = B * (12 + M * C * 4 + 12) + 2 * M * C * 4
+    return {"us_per_call": us, "batch": B, "samples_per_s": B / us * 1e6, "bytes_per_call": bb,
             "achieved_GBs": bb / us / 1e3, "frac": bb / us / 1e3 / HBM_PEAK_GBS,
+            "min_bytes_per_call": bmin, "frac_min_bytes": bmin / us / 1e3 / HBM_PEAK_GBS,
+            "kernel": "persistent (action_bwd_persist_kernel)" if plan["tile"] == 3 else
+                      "one group per block (action_bwd_tile_kernel)",
+            "blocks": plan["blocks"],
             "bytes_note": "angles + output gradient in, angle gradient out, F in / dF out, "
-                          "the dF slabs written and read once (workspace)"}
+                          "the dF slabs written and read once (one per block); "
+                          "min_bytes_per_call leaves the slabs out"}
 
 
 if __name__ == "__main__":
