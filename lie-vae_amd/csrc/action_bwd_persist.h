@@ -45,8 +45,18 @@ constexpr int kBwdVarPersistNW5 = 128;
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
+// Samples of the gradient tile sit kPersistStride(L) floats apart in LDS: M*C rounded up
+// to 10 mod 64 banks, so that the 10 column lanes of the 6 samples hit 60 distinct banks
+// (the unpadded 1,210 floats = 58 mod 64 made adjacent samples' lanes collide 2-way; the
+// counters showed 0.64 bank-conflict cycles per LDS instruction, r05_pmc_persist_65536).
+// (The pad is a multiple of 4 floats so that every sample keeps its global address mod 16
+// in LDS, which the 16-byte LDS-DMA pieces need.)
+__host__ __device__ constexpr int persist_stride(int L) {
+  return (L + 1) * (L + 1) * 10 + ((((10 - ((L + 1) * (L + 1) * 10) % 64) + 64) % 64 + 3) & ~3);
+}
+static_assert(persist_stride(10) == 1226, "l = 10: 1,210 + 16 floats (10 mod 64)");
 __host__ __device__ constexpr int persist_tile_floats(int L) {
-  return (((64 / 10) * (L + 1) * (L + 1) * 10 * 4 + 16 + 15) & ~15) / 4;
+  return (((64 / 10) * persist_stride(L) * 4 + 16 + 15) & ~15) / 4;
 }
 __host__ __device__ constexpr int persist_lds_floats(int L, int NW, int NB = 2) {
   return NB * persist_tile_floats(L) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
@@ -64,6 +74,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr int MC4 = (MC + 3) & ~3;
   constexpr int kRow = TrigLds<LT>::kRow;
   constexpr int kTile = persist_tile_floats(LT);
+  constexpr int kStride = persist_stride(LT);  // floats between samples of the tile
   constexpr int kTrig = Sw * kRow;
   constexpr int kAp = NW * 64 * 3;
   constexpr int nthr = 64 * NW;
@@ -91,22 +102,25 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   // all groups' tiles sit at the same offset mod 16 (Sw * MC * 4 = 29,040 B at l = 10)
   const int mis = (int)(reinterpret_cast<uintptr_t>(a.gout) & 15);
 
+  // the group's gradient tile, global -> LDS by LDS-DMA, one sample per wave in turn (the
+  // samples are kStride floats apart in LDS, contiguous in global memory): 16-byte pieces
+  // for each sample's 16-byte-aligned body, 4-byte pieces for its head and tail
   auto issue_tile = [&](int64_t g, int buf) {
     const int64_t s0 = g * Sw;
     const int Sv = (int)min((int64_t)Sw, n - s0);
-    const int nbytes = Sv * MC * 4;
-    const char* gb = reinterpret_cast<const char*>(a.gout + s0 * MC);
-    char* stage_b = reinterpret_cast<char*>(tiles + buf * kTile) + mis;
-    const int head = min((16 - mis) & 15, nbytes);
-    const int nvec = (nbytes - head) >> 4;
-    const int tail0 = head + nvec * 16;
-    for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
-      if (v0 + lane < nvec)
-        __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(stage_b + head + 16 * v0), 16, 0, 0);
-    if (wave == NW - 1) {
-      if (4 * lane < head) __builtin_amdgcn_global_load_lds(gb + 4 * lane, as_lds(stage_b), 4, 0, 0);
-      if (tail0 + 4 * lane < nbytes)
-        __builtin_amdgcn_global_load_lds(gb + tail0 + 4 * lane, as_lds(stage_b + tail0), 4, 0, 0);
+    for (int jj = wave; jj < Sv; jj += NW) {
+      const char* gb = reinterpret_cast<const char*>(a.gout + (s0 + jj) * MC);
+      char* sb = reinterpret_cast<char*>(tiles + buf * kTile + jj * kStride) + mis;
+      const int smis = (int)(reinterpret_cast<uintptr_t>(gb) & 15);
+      const int head = min((16 - smis) & 15, MC * 4);
+      const int nvec = (MC * 4 - head) >> 4;
+      const int tail0 = head + nvec * 16;
+      for (int v0 = 0; v0 < nvec; v0 += 64)
+        if (v0 + lane < nvec)
+          __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(sb + head + 16 * v0), 16, 0, 0);
+      if (4 * lane < head) __builtin_amdgcn_global_load_lds(gb + 4 * lane, as_lds(sb), 4, 0, 0);
+      if (tail0 + 4 * lane < MC * 4)
+        __builtin_amdgcn_global_load_lds(gb + tail0 + 4 * lane, as_lds(sb + tail0), 4, 0, 0);
     }
   };
   // the stored angle a task's slot uses (transpose: slot q takes angle 2 - q)
@@ -164,7 +178,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     const int Sv = (int)min((int64_t)Sw, n - s0);
     const bool active = j < Sv;
     char* stage_b = reinterpret_cast<char*>(tiles + tcur * kTile) + mis;
-    float* tile_lane = reinterpret_cast<float*>(stage_b) + j * MC + c;
+    float* tile_lane = reinterpret_cast<float*>(stage_b) + j * kStride + c;
     const float* tj = trig + cur * kTrig + min(j, Sw - 1) * kRow;
     float ga = 0.f, gb = 0.f, gc = 0.f;
     sfor<LT + 1>([&](auto Lc) {
@@ -223,7 +237,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
             for (int uu = 0; uu < kU; ++uu) {
               const int e = base + min(e0 + 64 * uu, cnt - 1);
 #pragma unroll
-              for (int jj = 0; jj < Sw; ++jj) v[uu][jj] = t0[jj * MC + e];
+              for (int jj = 0; jj < Sw; ++jj) v[uu][jj] = t0[jj * kStride + e];
             }
 #pragma unroll
             for (int uu = 0; uu < kU; ++uu) {
@@ -236,7 +250,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         } else {
           for (int e = lane; e < cnt; e += 64) {
             float sum = t0[base + e];
-            for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * MC + base + e];
+            for (int jj = 1; jj < Sv; ++jj) sum += t0[jj * kStride + base + e];
             slab[base + e] += sum;
           }
         }
