@@ -58,7 +58,13 @@ def main():
     e1.record(cur)
     torch.cuda.synchronize(dev)
     us = e0.elapsed_time(e1) * 1e3 / (reps * 50)
+    import hashlib
+    import numpy as np
+    gf = gF.cpu().numpy()
+    np.save(os.path.join(REPO, "gpurun_out", f"bwd_only_gF_{B}_{os.environ.get('LV_BWD_VARIANT', 'd')}.npy"), gf)
     print(json.dumps({"batch": B, "calls": reps * 50, "us_per_call": us,
+                      "gF_sha": hashlib.sha1(gf.tobytes()).hexdigest()[:12],
+                      "gang_sha": hashlib.sha1(gang.cpu().numpy().tobytes()).hexdigest()[:12],
                       "plan": _lib.plan("bwd", B, L, C, 1)}), flush=True)
 
 
