@@ -41,14 +41,6 @@ constexpr int kBwdVarSlabFlat = 2, kBwdVarSlabWT = 4;
 constexpr int kBwdVarSplit = 8;
 // prologue tasks spread over the block's waves (see action_bwd_tile_kernel)
 constexpr int kBwdVarSpread = 16;
-// dF straight from the chain's registers into the LDS slab by LDS float atomics
-// (ds_add_f32; a degree's rows belong to one wave, and the 6 samples of an address are
-// added in lane order), instead of the dF column written back into the gradient tile and
-// a per-group pass summing the 6 samples (one-group and persistent kernels)
-constexpr int kBwdVarAtomicSlab = 256;
-__device__ __forceinline__ void lds_add_f32(float* p, float v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 struct ActionBwdArgs {
   const float* ang;
   const float* F;
@@ -304,7 +296,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
       const int e = fbase + fstr * k;
       fv[k] = e < fcnt ? fsrc[e] : 0.f;
     }
-    if (LOOP || (FM == kBwdFShared && (a.variant & kBwdVarAtomicSlab)))
+    if constexpr (LOOP)
       each_degree([&](int l) {  // this wave's rows
         for (int e = lane; e < (2 * l + 1) * C; e += 64) slabL[l * l * C + e] = 0.f;
       });
@@ -454,12 +446,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
           sfor<nn>([&](auto K) { f0[LV_CV(K)] = fcol[LV_CV(K) * fst]; });
           gc += kdot<l>(u, f0);
         }
-        if (FM == kBwdFShared && !LOOP && (a.variant & kBwdVarAtomicSlab)) {
-          // dF straight into the LDS slab (ds_add_f32, the 6 samples of an address in lane order)
-          if (active) sfor<nn>([&](auto I) { lds_add_f32(slabL + (r0 + LV_CV(I)) * C + c, u[LV_CV(I)]); });
-        } else if (active) {
-          sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
-        }
+        if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
         if constexpr (SHAREDF && (LOOP || FM != kBwdFShared)) {
           // this degree's rows summed over the group's samples in sample order, added to
           // the block's slab (groups in order)
@@ -547,12 +534,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
           }
         }
       };
-      if (a.variant & kBwdVarAtomicSlab) {
-        // the LDS slab already holds the group's sums: this wave's rows to the workspace
-        each_degree([&](int l) {
-          for (int e = lane; e < (2 * l + 1) * C; e += 64) put(l * l * C + e, slabL[l * l * C + e]);
-        });
-      } else if (a.variant & kBwdVarSlabFlat) {
+      if (a.variant & kBwdVarSlabFlat) {
         // the wave's elements as one flat list over its degrees (ascending)
         int tot = 0;
         each_degree([&](int l) { tot += (2 * l + 1) * C; });

@@ -43,7 +43,6 @@ constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistNoJit = 64;
 // per-wave chain instead of ~0.85x of a 4-way split), built for 3 waves per SIMD
 constexpr int kBwdVarPersistNW5 = 128;
 
-
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
 // Samples of the gradient tile sit kPersistStride(L) floats apart in LDS: M*C rounded up
@@ -93,7 +92,6 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   const int j = lane / C;
   const int c = lane - j * C;
   const unsigned dmask = a.seg_mask[wave];
-  const bool atomic_slab = (a.variant & kBwdVarAtomicSlab) != 0;
   const int64_t P = gridDim.x;
   const int64_t groups = a.groups;
   const int64_t n = a.n;
@@ -220,17 +218,13 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
           sfor<nn>([&](auto K) { f0[LV_CV(K)] = fcol[LV_CV(K) * C]; });
           gc += kdot<l>(u, f0);
         }
-        if (atomic_slab) {
-          if (active) sfor<nn>([&](auto I) { lds_add_f32(slab + (r0 + LV_CV(I)) * C + c, u[LV_CV(I)]); });
-        } else if (active) {
-          sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
-        }
+        if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
       }
     });
     // 3. this wave's dF rows summed over the group's samples (sample order), added to the
     //    block's slab (groups in the block's order)
     wave_lds_sync();
-    if (!atomic_slab) {
+    {
       const float* t0 = reinterpret_cast<const float*>(stage_b);
       for (unsigned m = dmask; m; m &= m - 1) {
         const int l = __builtin_ctz(m);
