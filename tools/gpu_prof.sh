@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 TAG=$1; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-BENCH="bench.py --no-cpu-baseline --cold-launches 0 --multistream 1 --no-fwd-bwd --sweep= $*"
+BENCH="bench.py --no-cpu-baseline --cold-launches 0 --multistream 1 --no-fwd-bwd --config5-launches 0 --train-steps 0 --sweep= $*"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run() {  # name, timeout, cmd...
   local name=$1 t=$2; shift 2
