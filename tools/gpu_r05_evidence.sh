@@ -18,4 +18,7 @@ for B in 4096 65536; do
   step bwd_$B timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_bwd_only_$B -o run --output-format csv -- python3 tools/bwd_only.py $B
   rm -f gpurun_out/r05_bwd_only_$B/*kernel_trace.csv
 done
+# the N > 1 code path (config 4's DP train record, RCCL replaced by gloo because two ranks
+# share the box's one GPU): plumbing only, not scaling numbers
+step rehearse2 sh -c "LV_SHARE_GPU0=1 timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline --sweep= --cold-launches 0 > gpurun_out/r05_rehearse_2ranks.json 2> gpurun_out/r05_rehearse_2ranks.err"
 echo "=== all done"
