@@ -407,7 +407,10 @@ def test_action_bwd_persistent_kernel(gpu_device):
             (ops.group_action(ap, fp, L, transpose=transpose) * gout[lo:lo + 4096]).sum().backward()
             ga_parts.append(ap.grad)
             gf_sum += fp.grad.double()
-        assert_normwise(host(grads[0][0]), host(torch.cat(ga_parts)), 1e-5,
+        # per-sample angle gradients are sums of ~4,000 chain terms with cancellation; the
+        # chunks' plans (a ragged last chunk runs 8 degree sets) add them in another order:
+        # the suite's gradient tolerance
+        assert_normwise(host(grads[0][0]), host(torch.cat(ga_parts)), 1e-4,
                         what=f"persistent angle grads n={n}")
         assert_normwise(host(grads[0][1])[None], gf_sum.cpu().numpy()[None], 1e-5,
                         what=f"persistent dF n={n}")
