@@ -132,6 +132,14 @@ def main():
         dist.destroy_process_group()
 
 
+def _backend_name():
+    """The process group's transport: 'nccl' is RCCL over xGMI on ROCm; gloo only in the
+    one-GPU rehearsal (LV_SHARE_GPU0=1) and CPU tests."""
+    import torch.distributed as dist
+    b = dist.get_backend() if dist.is_initialized() else "none"
+    return "RCCL (nccl backend)" if b == "nccl" else b
+
+
 def time_train_steps(model, dev, world, rank, global_batch, steps, warmup, amp="off",
                      graph=False, fused_adam=True, flops=True):
     """Time `steps` DPTrainer steps (elbo fwd + bwd + bucketed all-reduce at world > 1 +
@@ -180,8 +188,8 @@ def time_train_steps(model, dev, world, rank, global_batch, steps, warmup, amp="
         "warmup_s": warm_s,
         "config": {"global_batch": global_batch, "per_gpu": B, "params": param_count(model),
                    "dtype": "f32" if amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
-                   "parallelism": (f"dp{world}: RCCL bucketed all-reduce of fp32 gradients"
-                                   if world > 1 else "single GPU"),
+                   "parallelism": (f"dp{world}: bucketed all-reduce of fp32 gradients over "
+                                   f"{_backend_name()}" if world > 1 else "single GPU"),
                    "launch": "graph" if graph else "eager"},
         "loss": float(loss.item()), "recon": float(recon.mean().item()),
         "kl": float(kl.mean().item())}
