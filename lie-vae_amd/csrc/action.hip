@@ -194,6 +194,49 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce4_kernel(const float* w
   }
 }
 
+// Chunk-major slabs, one 256-thread block per 16-element chunk (A/B LV_BWD_REDUCE=6):
+// thread t takes quarter q = t % 4 of slabs t / 4, t / 4 + 64, ... -- up to kR5Loads 16-byte
+// loads issued together per round -- then the 64 streams of a quarter are combined by
+// cross-lane shuffles inside each wave (xor 4, 8, 16, 32) and the 4 waves' partials in wave
+// order after one barrier.  Fewer threads and barriers than reduce3 (1,024 threads, an
+// 8-level tree); deterministic in a fixed order of its own.
+constexpr int kR5Loads = 12;
+__global__ __launch_bounds__(256) void action_bwd_reduce5_kernel(const float* ws_F, float* gF, int64_t MC, int nslab) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ f4 part[4][4];
+  const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
+  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)blockIdx.x * nslab * kSlabChunk) + q;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = bs; b0 < nslab; b0 += 64 * kR5Loads) {
+    f4 v[kR5Loads];
+#pragma unroll
+    for (int u = 0; u < kR5Loads; ++u) {
+      const int b = b0 + 64 * u;
+      v[u] = b < nslab ? base[(int64_t)b * 4] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kR5Loads; ++u) acc += v[u];
+  }
+#pragma unroll
+  for (int m = 4; m <= 32; m <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+  }
+  const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  if (lane < 4) part[w][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    f4 r = part[0][q];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) r += part[ww][q];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = (int64_t)blockIdx.x * kSlabChunk + 4 * q + k;
+      if (e < MC) gF[e] = r[k];
+    }
+  }
+}
+
 namespace {
 
 template <int... Ls>
@@ -702,7 +745,7 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // dF slab reduce: LV_BWD_REDUCE (A/B) 3 = chunk-major slabs + action_bwd_reduce3_kernel,
   // 16 / 8 / 4 = row slabs + action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
   static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
-  p.a.slab_chunked = b.fmode != kBwdFSample && (kEnvReduce == 3 || kEnvReduce == 5);
+  p.a.slab_chunked = b.fmode != kBwdFSample && (kEnvReduce == 3 || kEnvReduce == 5 || kEnvReduce == 6);
   static const int kEnvVariant = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
   p.a.variant = kEnvVariant;
   p.a.stamps = ab_stamps();
@@ -722,9 +765,14 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
     p.a.v = nullptr;
     p.a.mu = nullptr;
     if (int e = kBwdRun[L](p)) return e;
-    hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
-                       (const float*)workspace, gF, MC, b.gx, p.a.stamps);
-    LV_CHECK_LAUNCH("action_bwd_reduce3_kernel");
+    static const int kEnvReduceP = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
+    if (kEnvReduceP == 6)
+      hipLaunchKernelGGL(action_bwd_reduce5_kernel, dim3((unsigned)slab_chunks(MC)), dim3(256), 0, st,
+                         (const float*)workspace, gF, MC, b.gx);
+    else
+      hipLaunchKernelGGL(action_bwd_reduce3_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
+                         (const float*)workspace, gF, MC, b.gx, p.a.stamps);
+    LV_CHECK_LAUNCH("action_bwd_reduce_kernel");
     if (v) return lv_exp_eazyz_vjp(mu, v, p.a.gang, gmu, gv, n, st);
     return LV_OK;
   }
@@ -735,6 +783,11 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   // 4,096, 187 vs 191 at 65,536, 9.9 vs 9.8 at 512 against reduce2<16>, the round-3
   // default; an in-kernel reduction by the tile kernel's last blocks -- completion counter,
   // device-scope release fences -- ran 75 us per call at 4,096 and was dropped)
+  if (p.a.slab_chunked && kEnvReduce == 6) {
+    hipLaunchKernelGGL(action_bwd_reduce5_kernel, dim3((unsigned)slab_chunks(MC)), dim3(256), 0, st,
+                       (const float*)workspace, gF, MC, b.gx);
+    LV_RETURN_LAUNCH("action_bwd_reduce5_kernel");
+  }
   if (p.a.slab_chunked && kEnvReduce == 5) {
     hipLaunchKernelGGL(action_bwd_reduce4_kernel, dim3((unsigned)slab_chunks(MC)), dim3(1024), 0, st,
                        (const float*)workspace, gF, MC, b.gx);
