@@ -99,6 +99,10 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   const int t_task = lane * NW + wave;
   const bool task = t_task < 3 * Sw;
   const int jt = t_task / 3, q = t_task - 3 * (t_task / 3);
+  // A/B timeline (LV_STAMPS=1): phase stamps of the block's 5th group (steady state)
+  auto st = [&](int kk, int ph) {
+    if (kk == 4 && a.stamps) phase_stamp(a.stamps, wave, ph);
+  };
   // all groups' tiles sit at the same offset mod 16 (Sw * MC * 4 = 29,040 B at l = 10)
   const int mis = (int)(reinterpret_cast<uintptr_t>(a.gout) & 15);
 
@@ -168,6 +172,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     const int tcur = DB ? cur : 0;
     const int64_t gn = g + P;
     const bool has_next = gn < groups;
+    st(k, 0);
     // 1. next group's angle loads (task lanes), then (double buffer) its gradient tile by
     //    LDS-DMA; a single buffer is refilled after this group's barrier (step 7)
     if (task && has_next) ang_next = task_angle(gn);
@@ -221,6 +226,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
       }
     });
+    st(k, 1);
     // 3. this wave's dF rows summed over the group's samples (sample order), added to the
     //    block's slab (groups in the block's order)
     wave_lds_sync();
@@ -256,6 +262,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         }
       }
     }
+    st(k, 2);
     // 4. the next group's multiples (its angles have long landed)
     if (task && has_next) task_fill(ang_next, nxt);
     // 5. angle partials; the barrier also publishes the next tile (this wave's LDS-DMA
@@ -267,7 +274,9 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
       ap[lane * 3 + 0] = ga; ap[lane * 3 + 1] = gb; ap[lane * 3 + 2] = gc;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st(k, 3);
     block_sync_lds();
+    st(k, 4);
     // 6. the group's angle gradients (columns in order, then waves in order), output t on
     //    lane t / NW of wave t % NW: no wave carries all 18 serial 40-term sums into its
     //    next chain
@@ -288,9 +297,12 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     //    above), so the tile takes the next group now; its wait and barrier follow
     if constexpr (!DB) {
       if (has_next) {
+        st(k, 5);
         issue_tile(gn, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st(k, 6);
         block_sync_lds();
+        st(k, 7);
       }
     }
   }
