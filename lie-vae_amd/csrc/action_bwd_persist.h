@@ -263,42 +263,51 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
       }
     }
     st(k, 2);
-    // 4. the next group's multiples (its angles have long landed)
-    if (task && has_next) task_fill(ang_next, nxt);
-    // 5. angle partials; the barrier also publishes the next tile (this wave's LDS-DMA
-    //    share waited for here) and the next multiples
-    float* ap = apart + cur * kAp + wave * 64 * 3;
-    if (a.transpose) {
-      ap[lane * 3 + 0] = -gc; ap[lane * 3 + 1] = -gb; ap[lane * 3 + 2] = -ga;
-    } else {
-      ap[lane * 3 + 0] = ga; ap[lane * 3 + 1] = gb; ap[lane * 3 + 2] = gc;
+    // 4. (double buffer) the next group's multiples (its angles have long landed)
+    if (DB && task && has_next) task_fill(ang_next, nxt);
+    // 5. angle partials: the C column lanes of each sample summed by a segmented
+    //    cross-lane tree (((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7))) + (c8 + c9), then
+    //    one (sample, angle) value per wave into the partial buffer
+    {
+      float v0 = ga, v1 = gb, v2 = gc;
+#pragma unroll
+      for (int off = 1; off < C; off <<= 1) {
+        const float t0 = __shfl_down(v0, off, 64), t1 = __shfl_down(v1, off, 64), t2 = __shfl_down(v2, off, 64);
+        if ((c & (2 * off - 1)) == 0 && c + off < C) {
+          v0 += t0;
+          v1 += t1;
+          v2 += t2;
+        }
+      }
+      if (c == 0 && j < Sw) {
+        float* ap = apart + cur * kAp + (wave * Sw + j) * 3;
+        if (a.transpose) {
+          ap[0] = -v2; ap[1] = -v1; ap[2] = -v0;
+        } else {
+          ap[0] = v0; ap[1] = v1; ap[2] = v2;
+        }
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (DB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the next tile
     st(k, 3);
     block_sync_lds();
     st(k, 4);
-    // 6. the group's angle gradients (columns in order, then waves in order), output t on
-    //    lane t / NW of wave t % NW: no wave carries all 18 serial 40-term sums into its
-    //    next chain
+    // 6. (one buffer) every wave is past this group's chain and slab pass: the tile takes
+    //    the next group now, and the angle sums and the next multiples run under its DMA
+    if (!DB && has_next) issue_tile(gn, 0);
+    // 7. the group's angle gradients (waves in order), output t on lane t / NW of wave t % NW
     if (t_task < 3 * Sv) {
       const int js = t_task / 3, i = t_task - 3 * (t_task / 3);
       const float* apc = apart + cur * kAp;
-      float r = 0.f;
+      float r = apc[js * 3 + i];
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        float sw = 0.f;
-#pragma unroll
-        for (int cc = 0; cc < C; ++cc) sw += apc[(w * 64 + js * C + cc) * 3 + i];
-        r += sw;
-      }
+      for (int w = 1; w < NW; ++w) r += apc[(w * Sw + js) * 3 + i];
       a.gang[(s0 + js) * 3 + i] = r;
     }
-    // 7. single buffer: every wave is past this group's chain and slab pass (the barrier
-    //    above), so the tile takes the next group now; its wait and barrier follow
     if constexpr (!DB) {
       if (has_next) {
+        if (task) task_fill(ang_next, nxt);
         st(k, 5);
-        issue_tile(gn, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st(k, 6);
         block_sync_lds();

@@ -40,7 +40,7 @@ def main():
     buf = np.zeros(16384 * 16 * 8, dtype=np.uint64)
     got = f(buf.ctypes.data, buf.nbytes)
     st = buf[: nblk * 16 * 8].reshape(nblk, 16, 8).astype(np.int64)
-    names = ["chain", "slab pass", "fill+partials", "barrier B", "gang sums", "tile DMA wait", "barrier A"]
+    names = ["chain", "slab pass", "partials", "barrier B", "DMA issue+gang sums+fill", "tile DMA wait", "barrier A"]
     print(f"persistent backward B={B}: {nblk} blocks, phase durations of the 5th group (median / p90 us)")
     for w in range(4):
         s = st[:, w, :]
