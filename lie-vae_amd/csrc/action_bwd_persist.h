@@ -167,6 +167,11 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   block_sync_lds();
 
   const float* Fl = Fsp + c;
+  // the flat slab pass (step 3): this wave's element pairs, the tile's 8-byte alignment
+  constexpr int kPR = 3;
+  int npairs = 0;
+  for (unsigned m = dmask; m; m &= m - 1) npairs += 5 * (2 * __builtin_ctz(m) + 1);
+  const bool pair_ok = (mis & 7) == 0 && npairs <= 64 * kPR;
   for (int k = 0; g < groups; ++k, g += P) {
     const int cur = k & 1, nxt = cur ^ 1;
     const int tcur = DB ? cur : 0;
@@ -230,7 +235,38 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     // 3. this wave's dF rows summed over the group's samples (sample order), added to the
     //    block's slab (groups in the block's order)
     wave_lds_sync();
-    {
+    if (pair_ok && Sv == Sw) {
+      // full group, 8-byte aligned tile: the wave's rows as ONE flat list of element pairs
+      // (a degree's 10 (2l+1) elements are whole pairs), up to kPR rounds of 64 pairs with
+      // every 8-byte load issued before any sum: one LDS round trip for the loads, one for
+      // the slab's read-modify-write (the per-degree passes took 3-6)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const float* t0 = reinterpret_cast<const float*>(stage_b);
+      f2 v[kPR][Sw];
+      int off[kPR];
+#pragma unroll
+      for (int uu = 0; uu < kPR; ++uu) {
+        const int pp = lane + 64 * uu;
+        int o = 0, acc = 0;
+        for (unsigned m = dmask; m; m &= m - 1) {
+          const int l = __builtin_ctz(m);
+          const int np = 5 * (2 * l + 1);
+          if (pp >= acc && pp < acc + np) o = l * l * C + 2 * (pp - acc);
+          acc += np;
+        }
+        off[uu] = pp < npairs ? o : -1;
+#pragma unroll
+        for (int jj = 0; jj < Sw; ++jj)
+          v[uu][jj] = *reinterpret_cast<const f2*>(t0 + jj * kStride + (off[uu] < 0 ? 0 : off[uu]));
+      }
+#pragma unroll
+      for (int uu = 0; uu < kPR; ++uu) {
+        f2 sum = v[uu][0];
+#pragma unroll
+        for (int jj = 1; jj < Sw; ++jj) sum += v[uu][jj];
+        if (off[uu] >= 0) *reinterpret_cast<f2*>(slab + off[uu]) += sum;
+      }
+    } else {
       const float* t0 = reinterpret_cast<const float*>(stage_b);
       for (unsigned m = dmask; m; m &= m - 1) {
         const int l = __builtin_ctz(m);
