@@ -45,16 +45,13 @@ constexpr int kBwdVarPersistNW5 = 128;
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
-// Samples of the gradient tile sit kPersistStride(L) floats apart in LDS: M*C rounded up
-// to 10 mod 64 banks, so that the 10 column lanes of the 6 samples hit 60 distinct banks
-// (the unpadded 1,210 floats = 58 mod 64 made adjacent samples' lanes collide 2-way; the
-// counters showed 0.64 bank-conflict cycles per LDS instruction, r05_pmc_persist_65536).
-// (The pad is a multiple of 4 floats so that every sample keeps its global address mod 16
-// in LDS, which the 16-byte LDS-DMA pieces need.)
-__host__ __device__ constexpr int persist_stride(int L) {
-  return (L + 1) * (L + 1) * 10 + ((((10 - ((L + 1) * (L + 1) * 10) % 64) + 64) % 64 + 3) & ~3);
-}
-static_assert(persist_stride(10) == 1226, "l = 10: 1,210 + 16 floats (10 mod 64)");
+// Samples of the gradient tile sit M*C floats apart in LDS, exactly as in global memory, so
+// one LDS-DMA instruction moves 1 KiB of any sample(s) and the tile takes ~29 of them,
+// spread evenly over the waves.  (Padding each sample to 10 mod 64 banks removed the 2-way
+// conflicts between adjacent samples' lanes -- 0.64 conflict cycles per LDS instruction at
+// 65,536 -- but needs per-sample DMA with head / tail pieces: twice the DMA instructions,
+// ~0.05 us of issue each; 109.7 -> 109.0 us, dropped for the flat slab pass below.)
+__host__ __device__ constexpr int persist_stride(int L) { return (L + 1) * (L + 1) * 10; }
 __host__ __device__ constexpr int persist_tile_floats(int L) {
   return (((64 / 10) * persist_stride(L) * 4 + 16 + 15) & ~15) / 4;
 }
@@ -106,25 +103,24 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   // all groups' tiles sit at the same offset mod 16 (Sw * MC * 4 = 29,040 B at l = 10)
   const int mis = (int)(reinterpret_cast<uintptr_t>(a.gout) & 15);
 
-  // the group's gradient tile, global -> LDS by LDS-DMA, one sample per wave in turn (the
-  // samples are kStride floats apart in LDS, contiguous in global memory): 16-byte pieces
-  // for each sample's 16-byte-aligned body, 4-byte pieces for its head and tail
+  // the group's gradient tile, global -> LDS by LDS-DMA: 16-byte pieces (1 KiB per wave
+  // instruction) spread over the waves, 4-byte head / tail pieces
   auto issue_tile = [&](int64_t g, int buf) {
     const int64_t s0 = g * Sw;
     const int Sv = (int)min((int64_t)Sw, n - s0);
-    for (int jj = wave; jj < Sv; jj += NW) {
-      const char* gb = reinterpret_cast<const char*>(a.gout + (s0 + jj) * MC);
-      char* sb = reinterpret_cast<char*>(tiles + buf * kTile + jj * kStride) + mis;
-      const int smis = (int)(reinterpret_cast<uintptr_t>(gb) & 15);
-      const int head = min((16 - smis) & 15, MC * 4);
-      const int nvec = (MC * 4 - head) >> 4;
-      const int tail0 = head + nvec * 16;
-      for (int v0 = 0; v0 < nvec; v0 += 64)
-        if (v0 + lane < nvec)
-          __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(sb + head + 16 * v0), 16, 0, 0);
-      if (4 * lane < head) __builtin_amdgcn_global_load_lds(gb + 4 * lane, as_lds(sb), 4, 0, 0);
-      if (tail0 + 4 * lane < MC * 4)
-        __builtin_amdgcn_global_load_lds(gb + tail0 + 4 * lane, as_lds(sb + tail0), 4, 0, 0);
+    const int nbytes = Sv * MC * 4;
+    const char* gb = reinterpret_cast<const char*>(a.gout + s0 * MC);
+    char* stage_b = reinterpret_cast<char*>(tiles + buf * kTile) + mis;
+    const int head = min((16 - mis) & 15, nbytes);
+    const int nvec = (nbytes - head) >> 4;
+    const int tail0 = head + nvec * 16;
+    for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
+      if (v0 + lane < nvec)
+        __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(stage_b + head + 16 * v0), 16, 0, 0);
+    if (wave == NW - 1) {
+      if (4 * lane < head) __builtin_amdgcn_global_load_lds(gb + 4 * lane, as_lds(stage_b), 4, 0, 0);
+      if (tail0 + 4 * lane < nbytes)
+        __builtin_amdgcn_global_load_lds(gb + tail0 + 4 * lane, as_lds(stage_b + tail0), 4, 0, 0);
     }
   };
   // the stored angle a task's slot uses (transpose: slot q takes angle 2 - q)
@@ -134,8 +130,10 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     return a.ang[(s0 + min(jt, Sv - 1)) * 3 + (a.transpose ? 2 - q : q)];
   };
   auto task_fill = [&](float ang, int buf) {
+    // straight-line sincos (Cody-Waite + minimax, <= 1.6 ulp; action_common.h): the
+    // library sincosf's range-reduction branches sat on every group's prologue path
     float cq, sq;
-    sincosf(ang, &sq, &cq);
+    lv_sincos(ang, sq, cq);
     if (a.transpose) sq = -sq;
     trig_row_fill1<LT>(trig + buf * kTrig + jt * kRow, cq, sq, q, LT);
   };
