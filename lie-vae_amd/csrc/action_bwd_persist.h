@@ -89,8 +89,6 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   const int j = lane / C;
   const int c = lane - j * C;
   const unsigned dmask = a.seg_mask[wave];
-  // (one buffer) the first degree's forward recompute ahead of the tile's wait and barrier
-  const bool split = (a.variant & kBwdVarSplit) != 0;
   const int64_t P = gridDim.x;
   const int64_t groups = a.groups;
   const int64_t n = a.n;
@@ -191,10 +189,6 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     float* tile_lane = reinterpret_cast<float*>(stage_b) + j * kStride + c;
     const float* tj = trig + cur * kTrig + min(j, Sw - 1) * kRow;
     float ga = 0.f, gb = 0.f, gc = 0.f;
-    // one buffer: this group's tile was issued after the previous group's barrier; the first
-    // degree's forward recompute (P1..P4: the multiples and the spectrum, not the tile) runs
-    // before its wait and barrier
-    bool split_pending = !DB && k > 0 && split;
     sfor<LT + 1>([&](auto Lc) {
       constexpr int l = LT - LV_CV(Lc);
       if ((dmask >> l) & 1u) {
@@ -212,13 +206,6 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         jmul<l>(u, p2);                                                    // P2
         xm<l>(mult_lds<l, 1, LT>(tj), p2, u);                              // P3
         jmul<l>(u, p4);                                                    // P4
-        if (split_pending) {  // the tile: this wave's DMA share, then everyone's
-          st(k, 6);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          block_sync_lds();
-          st(k, 7);
-          split_pending = false;
-        }
         if constexpr (JIT) {
           xm_mem<l, true>(mult_lds<l, 0, LT>(tj), tile_lane + r0 * C, C, u);  // Q4
         } else {
@@ -242,10 +229,6 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         if (active) sfor<nn>([&](auto I) { tile_lane[(r0 + LV_CV(I)) * C] = u[LV_CV(I)]; });
       }
     });
-    if (split_pending) {  // a wave without degrees still takes the tile barrier
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      block_sync_lds();
-    }
     st(k, 1);
     // 3. this wave's dF rows summed over the group's samples (sample order), added to the
     //    block's slab (groups in the block's order)
@@ -314,8 +297,8 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
       }
     }
     st(k, 2);
-    // 4. the next group's multiples (its angles have long landed)
-    if (task && has_next) task_fill(ang_next, nxt);
+    // 4. (double buffer) the next group's multiples (its angles have long landed)
+    if (DB && task && has_next) task_fill(ang_next, nxt);
     // 5. angle partials: the C column lanes of each sample summed by a segmented
     //    cross-lane tree (((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7))) + (c8 + c9), then
     //    one (sample, angle) value per wave into the partial buffer
@@ -344,8 +327,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     block_sync_lds();
     st(k, 4);
     // 6. (one buffer) every wave is past this group's chain and slab pass: the tile takes
-    //    the next group now; the angle sums and the next group's first forward recompute
-    //    run under its DMA (the wait and barrier sit in that chain)
+    //    the next group now, and the angle sums and the next multiples run under its DMA
     if (!DB && has_next) issue_tile(gn, 0);
     // 7. the group's angle gradients (waves in order), output t on lane t / NW of wave t % NW
     if (t_task < 3 * Sv) {
@@ -356,10 +338,15 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
       for (int w = 1; w < NW; ++w) r += apc[(w * Sw + js) * 3 + i];
       a.gang[(s0 + js) * 3 + i] = r;
     }
-    st(k, 5);
-    if (!DB && !split && has_next) {  // the tile's wait and barrier here instead
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      block_sync_lds();
+    if constexpr (!DB) {
+      if (has_next) {
+        if (task) task_fill(ang_next, nxt);
+        st(k, 5);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st(k, 6);
+        block_sync_lds();
+        st(k, 7);
+      }
     }
   }
   // ---- the block's slab (each wave its own rows) to the workspace, chunk-major

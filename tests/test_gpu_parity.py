@@ -368,7 +368,9 @@ def test_action_bwd_reproducible_and_looped(gpu_device):
         (ops.group_action(ap, fp, L) * gout[lo:lo + 4096]).sum().backward()
         ga_parts.append(ap.grad)
         gf_sum += fp.grad.double()
-    assert_normwise(host(a.grad), host(torch.cat(ga_parts)), 1e-5, what="looped angle grads")
+    # one plan (persistent, 8,334 groups) vs 4,096-sample chunks (one-group kernel): the
+    # same per-sample sums in different orders (column tree, degree split over waves)
+    assert_normwise(host(a.grad), host(torch.cat(ga_parts)), 1e-4, what="looped angle grads")
     assert_normwise(host(f.grad)[None], gf_sum.cpu().numpy()[None], 1e-5, what="looped dF")
 
 

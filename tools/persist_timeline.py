@@ -40,19 +40,15 @@ def main():
     buf = np.zeros(16384 * 16 * 8, dtype=np.uint64)
     got = f(buf.ctypes.data, buf.nbytes)
     st = buf[: nblk * 16 * 8].reshape(nblk, 16, 8).astype(np.int64)
-    # stamp order in the loop: 0 top, 6 first forward recompute done, 7 tile barrier passed,
-    # 1 chain done, 2 slab pass done, 3 multiples + partials done, 4 group barrier passed,
-    # 5 DMA issued + angle sums done
-    order = [0, 6, 7, 1, 2, 3, 4, 5]
-    names = ["first P1..P4", "tile wait+barrier", "rest of chain", "slab pass", "fill+partials",
-             "group barrier", "DMA issue+gang sums"]
+    names = ["chain", "slab pass", "partials", "barrier B", "DMA issue+gang sums+fill", "tile DMA wait", "barrier A"]
+    print(f"persistent backward B={B}: {nblk} blocks, phase durations of the 5th group (median / p90 us)")
     for w in range(4):
-        s = st[:, w, :][:, order]
-        ok = (s > 0).all(axis=1)
+        s = st[:, w, :]
+        ok = (s[:, 0] > 0) & (s[:, 7] > 0)
         d = np.diff(s[ok], axis=1) * 0.01  # 100 MHz -> us
         row = "  ".join(f"{n} {np.median(d[:, i]):.2f}/{np.percentile(d[:, i], 90):.2f}" for i, n in enumerate(names))
         print(f"  wave {w}: {row}  (n={ok.sum()})")
-    tot = (st[:, 0, 5] - st[:, 0, 0]) * 0.01
+    tot = (st[:, 0, 7] - st[:, 0, 0]) * 0.01
     tot = tot[tot > 0]
     print(f"  group total (wave 0): median {np.median(tot):.2f} us")
 
