@@ -573,8 +573,9 @@ constexpr int64_t kBwdCUs = 256;  // MI355X compute units
 constexpr int kBwdReduceDefault = 3;  // LV_BWD_REDUCE default (see action_bwd_common)
 // LV_BWD_VARIANT default (kBwdVar* bits): JIT chain (profiles/r04_bwd_reduce_ab.txt); the
 // persistent kernel with one tile buffer at 3 blocks per CU (65,536: 131 -> 114 us against
-// the double-buffered 2 blocks per CU, profiles/r05_ab4.txt)
-constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle;
+// the double-buffered 2 blocks per CU, profiles/r05_ab4.txt), its next multiples filled by
+// one wave (profiles/r05_ab8.txt)
+constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1;
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
@@ -619,7 +620,6 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       b.groups = groups;
       static const int kEnvVariantP = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
       const bool single = (kEnvVariantP & kBwdVarPersistSingle) != 0;  // A/B: one tile buffer
-      if (kEnvVariantP & kBwdVarPersistNW5) b.nseg = 5;                 // A/B: 5 waves per block
       b.gx = (int)std::min<int64_t>(groups, kBwdCUs * (single ? 3 : kBwdPersistBlocksPerCU));
       plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
       balance_masks(L, b.nseg, true, b.seg_mask);

@@ -635,15 +635,8 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
   if (p.persist) {
     if constexpr (LT <= kBwdPersistMaxL) {
       const bool single = (p.a.variant & kBwdVarPersistSingle) != 0;
-      const bool nojit = (p.a.variant & kBwdVarPersistNoJit) != 0;
-      if (p.nseg == 5)
-        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, 5, true, true, 3>), grid, block, p.lds, p.stream, p.a);
-      else if (single && nojit)
-        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, false>), grid, block, p.lds, p.stream, p.a);
-      else if (single)
+      if (single)
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true>), grid, block, p.lds, p.stream, p.a);
-      else if (nojit)
-        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, true, false>), grid, block, p.lds, p.stream, p.a);
       else
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves>), grid, block, p.lds, p.stream, p.a);
     }

@@ -36,12 +36,13 @@ constexpr int kBwdPersistWaves = 4;      // degree-set waves per block
 constexpr int kBwdPersistBlocksPerCU = 2;
 // A/B variant bits of the persistent kernel (ActionBwdArgs::variant, A/B build only):
 // single gradient-tile buffer at 3 blocks per CU (3 waves per SIMD; the next tile is
-// loaded after the group's barrier), and the non-JIT chain (spectrum / gradient columns
-// read into registers at each product)
-constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistNoJit = 64;
-// ... and 5 degree-set waves per block (10 per CU: the l = 10 set is then ~1.1x the mean
-// per-wave chain instead of ~0.85x of a 4-way split), built for 3 waves per SIMD
-constexpr int kBwdVarPersistNW5 = 128;
+// loaded after the group's barrier); the next group's multiples filled by the 18 first lanes
+// of the last wave instead of 4-5 lanes of every wave (every wave then ran the whole
+// sincos + recurrence; 65,536: 110.3 -> 107.9 us, 262,144: 390 -> 376 us; both are the
+// product default).  (The non-JIT chain, 5 waves per block and one buffer at 2 blocks per
+// CU built for 2 waves per SIMD were slower: profiles/r05_bwd_persist_ab2.txt, r05_ab4.txt,
+// r05_ab8.txt.)
+constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistTask1 = 512;
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
@@ -92,10 +93,12 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   const int64_t P = gridDim.x;
   const int64_t groups = a.groups;
   const int64_t n = a.n;
-  // prologue task of this thread: task t = lane * NW + wave (spread over the waves)
+  // prologue task of this thread: task t = lane * NW + wave (spread over the waves), or
+  // (A/B) t = lane of the last wave; the angle sums (step 7) keep the spread numbering
   const int t_task = lane * NW + wave;
-  const bool task = t_task < 3 * Sw;
-  const int jt = t_task / 3, q = t_task - 3 * (t_task / 3);
+  const int t_fill = (a.variant & kBwdVarPersistTask1) ? (wave == NW - 1 ? lane : 64) : t_task;
+  const bool task = t_fill < 3 * Sw;
+  const int jt = t_fill / 3, q = t_fill - 3 * (t_fill / 3);
   // A/B timeline (LV_STAMPS=1): phase stamps of the block's 5th group (steady state)
   auto st = [&](int kk, int ph) {
     if (kk == 4 && a.stamps) phase_stamp(a.stamps, wave, ph);
@@ -170,6 +173,20 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   int npairs = 0;
   for (unsigned m = dmask; m; m &= m - 1) npairs += 5 * (2 * __builtin_ctz(m) + 1);
   const bool pair_ok = (mis & 7) == 0 && npairs <= 64 * kPR;
+  // this lane's pair offsets in the wave's rows (-1: none), fixed for the whole walk
+  int poff[kPR];
+#pragma unroll
+  for (int uu = 0; uu < kPR; ++uu) {
+    const int pp = lane + 64 * uu;
+    int o = 0, acc = 0;
+    for (unsigned m = dmask; m; m &= m - 1) {
+      const int l = __builtin_ctz(m);
+      const int np = 5 * (2 * l + 1);
+      if (pp >= acc && pp < acc + np) o = l * l * C + 2 * (pp - acc);
+      acc += np;
+    }
+    poff[uu] = pp < npairs ? o : -1;
+  }
   for (int k = 0; g < groups; ++k, g += P) {
     const int cur = k & 1, nxt = cur ^ 1;
     const int tcur = DB ? cur : 0;
@@ -241,18 +258,9 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
       typedef float f2 __attribute__((ext_vector_type(2)));
       const float* t0 = reinterpret_cast<const float*>(stage_b);
       f2 v[kPR][Sw];
-      int off[kPR];
+      const int* off = poff;
 #pragma unroll
       for (int uu = 0; uu < kPR; ++uu) {
-        const int pp = lane + 64 * uu;
-        int o = 0, acc = 0;
-        for (unsigned m = dmask; m; m &= m - 1) {
-          const int l = __builtin_ctz(m);
-          const int np = 5 * (2 * l + 1);
-          if (pp >= acc && pp < acc + np) o = l * l * C + 2 * (pp - acc);
-          acc += np;
-        }
-        off[uu] = pp < npairs ? o : -1;
 #pragma unroll
         for (int jj = 0; jj < Sw; ++jj)
           v[uu][jj] = *reinterpret_cast<const f2*>(t0 + jj * kStride + (off[uu] < 0 ? 0 : off[uu]));
