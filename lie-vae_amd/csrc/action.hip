@@ -194,7 +194,7 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce4_kernel(const float* w
   }
 }
 
-// Chunk-major slabs, one 256-thread block per 16-element chunk (A/B LV_BWD_REDUCE=6):
+// Chunk-major slabs, one 256-thread block per 16-element chunk (the default, LV_BWD_REDUCE=6):
 // thread t takes quarter q = t % 4 of slabs t / 4, t / 4 + 64, ... -- up to kR5Loads 16-byte
 // loads issued together per round -- then the 64 streams of a quarter are combined by
 // cross-lane shuffles inside each wave (xor 4, 8, 16, 32) and the 4 waves' partials in wave
@@ -570,7 +570,12 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 // profiles/r02_bwd_regbudget_sweep.txt).
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
 constexpr int64_t kBwdCUs = 256;  // MI355X compute units
-constexpr int kBwdReduceDefault = 3;  // LV_BWD_REDUCE default (see action_bwd_common)
+// LV_BWD_REDUCE default (see action_bwd_common): 6 = chunk-major slabs + reduce5 (one
+// 256-thread block per 16-element chunk).  Same box, backward alone (profiles/r05_reduce_ab.txt):
+// 512: 8.93 -> 8.72 us, 4,096: 14.45 -> 13.94, 16,384: 32.2 -> 31.9, 65,536: 103.4 -> 102.5
+// against reduce3; a block per quarter chunk (4x the blocks, 16-byte reads at a 64-byte
+// stride) was slower: 4,096: 17.2 us.
+constexpr int kBwdReduceDefault = 6;
 // LV_BWD_VARIANT default (kBwdVar* bits): JIT chain (profiles/r04_bwd_reduce_ab.txt); the
 // persistent kernel with one tile buffer at 3 blocks per CU (65,536: 131 -> 114 us against
 // the double-buffered 2 blocks per CU, profiles/r05_ab4.txt), its next multiples filled by
@@ -742,8 +747,9 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   p.a.fpitch = b.fpitch;
   static const int kEnvBwdPrio = LV_KNOB("LV_BWD_PRIO", 0);  // A/B: 2 = prologue-priority phases
   p.a.prio = kEnvBwdPrio;
-  // dF slab reduce: LV_BWD_REDUCE (A/B) 3 = chunk-major slabs + action_bwd_reduce3_kernel,
-  // 16 / 8 / 4 = row slabs + action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
+  // dF slab reduce: LV_BWD_REDUCE (A/B) 6 = chunk-major slabs + action_bwd_reduce5_kernel
+  // (default), 3 / 5 = the same slabs + reduce3 / reduce4, 16 / 8 / 4 = row slabs +
+  // action_bwd_reduce2_kernel<COLS>, 1 = the round-2 kernel
   static const int kEnvReduce = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
   p.a.slab_chunked = b.fmode != kBwdFSample && (kEnvReduce == 3 || kEnvReduce == 5 || kEnvReduce == 6);
   static const int kEnvVariant = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
@@ -778,8 +784,8 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
   }
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
-  // dF slab reduce: chunk-major slabs + action_bwd_reduce3_kernel by default
-  // (profiles/r04_bwd_reduce_ab.txt: 16.0 vs 18.0 us per lv_group_action_bwd call at batch
+  // dF slab reduce: chunk-major slabs + action_bwd_reduce5_kernel by default (kBwdReduceDefault;
+  // reduce3 before it, profiles/r04_bwd_reduce_ab.txt: 16.0 vs 18.0 us per lv_group_action_bwd call at batch
   // 4,096, 187 vs 191 at 65,536, 9.9 vs 9.8 at 512 against reduce2<16>, the round-3
   // default; an in-kernel reduction by the tile kernel's last blocks -- completion counter,
   // device-scope release fences -- ran 75 us per call at 4,096 and was dropped)
