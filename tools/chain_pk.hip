@@ -290,6 +290,106 @@ void chainP_kernel(const float* gtrig, const float* gF, const float* gtile, floa
   out[blockIdx.x * 256 + tid] = ga + gb + gc;
 }
 
+// ---- forward chain (X(c) F -> J -> X(b) -> J -> X(a)), degrees 0..20, 8 waves per block at
+// 2 blocks per CU (config 5's shape); scalar vs pair layout with the sines stored as
+// interleaved (s, -s) pairs so that each X pair is v_pk_mul_f32 + v_pk_fma_f32 from
+// compiler intrinsics (op_sel folds the swap and the cosine splat).
+constexpr int LT2 = 20, MC2 = (LT2 + 1) * (LT2 + 1) * C;
+constexpr int TP2 = TrigLds<LT2>::TP;
+constexpr int kRowS = 6 * TP2 + 4, kRowP = 9 * TP2 + 4;
+
+template <int l, int A>
+__device__ __forceinline__ void xrotS(const float* tj, const float (&x)[2 * l + 1], float (&y)[2 * l + 1]) {
+  float cc[l + 1], ss[l + 1];
+  sfor<(l + 4) / 4>([&](auto K) {
+    constexpr int k4 = LV_CV(K);
+    const f4 cv = *reinterpret_cast<const f4*>(tj + 2 * A * TP2 + 4 * k4);
+    const f4 sv = *reinterpret_cast<const f4*>(tj + (2 * A + 1) * TP2 + 4 * k4);
+    sfor<4>([&](auto I) {
+      constexpr int f = 4 * k4 + LV_CV(I);
+      if constexpr (f <= l) { cc[f] = cv[LV_CV(I)]; ss[f] = sv[LV_CV(I)]; }
+    });
+  });
+  sfor<l>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    y[i] = fmaf(cc[f], x[i], ss[f] * x[2 * l - i]);
+    y[2 * l - i] = fmaf(cc[f], x[2 * l - i], -(ss[f] * x[i]));
+  });
+  y[l] = x[l];
+}
+// pair layout: slot A's cosines at 3*A*TP, its (s, -s) pairs at 3*A*TP + TP
+template <int l, int A>
+__device__ __forceinline__ void xrotP2(const float* tj, const VP<l>& x, VP<l>& y) {
+  f4 cv[(l + 4) / 4];
+  f4 sn[(2 * l + 5) / 4];
+  sfor<(l + 4) / 4>([&](auto K) { cv[LV_CV(K)] = *reinterpret_cast<const f4*>(tj + 3 * A * TP2 + 4 * LV_CV(K)); });
+  sfor<(2 * l + 5) / 4>([&](auto K) { sn[LV_CV(K)] = *reinterpret_cast<const f4*>(tj + 3 * A * TP2 + TP2 + 4 * LV_CV(K)); });
+  sfor<l>([&](auto I) {
+    constexpr int i = LV_CV(I);
+    constexpr int f = l - i;
+    const float c = cv[f / 4][f % 4];
+    const f4 s4 = sn[(2 * f) / 4];
+    const f2 sp = (f & 1) ? s4.zw : s4.xy;
+    const f2 sw = __builtin_shufflevector(x.p[i], x.p[i], 1, 0);
+    y.p[i] = __builtin_elementwise_fma((f2)(c), x.p[i], sp * sw);
+  });
+  y.m = x.m;
+}
+
+template <bool PAIR>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void fwd_kernel(const float* gtrig, const float* gF, float* out, int reps, unsigned dmask) {
+  constexpr int kRow = PAIR ? kRowP : kRowS;
+  __shared__ __attribute__((aligned(16))) float trig[6 * kRowP];
+  __shared__ __attribute__((aligned(16))) float Fs[MC2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < 6 * kRowP; e += 512) trig[e] = gtrig[e % 64];
+  for (int e = tid; e < MC2; e += 512) Fs[e] = gF[e % MC];
+  __syncthreads();
+  const int j = min(lane / C, 5), c = lane % C;
+  const float* tj = trig + j * kRow;
+  const float* Fl = Fs + c;
+  float acc = 0.f;
+  // degrees spread over the 8 waves by cost: wave w takes l with (l * 7) % 8 == w (a fixed mix)
+  const unsigned wm = dmask & [&] { unsigned m = 0; for (int l = 0; l <= LT2; ++l) if ((l * 5 + l / 8) % 8 == wave) m |= 1u << l; return m; }();
+  for (int r = 0; r < reps; ++r) {
+    asm volatile("" : "+v"(tj), "+v"(Fl));
+    sfor<LT2 + 1>([&](auto Lc) {
+      constexpr int l = LV_CV(Lc);
+      constexpr int nn = 2 * l + 1, r0 = l * l;
+      if (!((wm >> l) & 1u)) return;
+      if constexpr (l == 0) {
+        acc += Fl[0];
+      } else if constexpr (PAIR) {
+        VP<l> x, y;
+        sfor<l>([&](auto I) { x.p[LV_CV(I)] = f2{Fl[(r0 + LV_CV(I)) * C], Fl[(r0 + 2 * l - LV_CV(I)) * C]}; });
+        x.m = Fl[(r0 + l) * C];
+        xrotP2<l, 2>(tj, x, y);
+        jmulP<l>(y, x);
+        xrotP2<l, 1>(tj, x, y);
+        jmulP<l>(y, x);
+        xrotP2<l, 0>(tj, x, y);
+        float sacc = y.m;
+        sfor<l>([&](auto I) { sacc += y.p[LV_CV(I)].x * y.p[LV_CV(I)].y; });
+        acc += sacc;
+      } else {
+        float x[nn], y[nn];
+        sfor<nn>([&](auto K) { x[LV_CV(K)] = Fl[(r0 + LV_CV(K)) * C]; });
+        xrotS<l, 2>(tj, x, y);
+        jmul<l>(y, x);
+        xrotS<l, 1>(tj, x, y);
+        jmul<l>(y, x);
+        xrotS<l, 0>(tj, x, y);
+        float sacc = y[l];
+        sfor<l>([&](auto I) { sacc += y[LV_CV(I)] * y[2 * l - LV_CV(I)]; });
+        acc += sacc;
+      }
+    });
+  }
+  out[blockIdx.x * 512 + tid] = acc;
+}
+
 int main() {
   std::vector<float> trig(12 * kRow), F(MC), tile(MC);
   for (size_t i = 0; i < trig.size(); ++i) trig[i] = 0.1f + 0.01f * (float)(i % 29);
@@ -325,6 +425,24 @@ int main() {
   run(chain_kernel<1, 2>, 512, 240, "float  (1 col/lane, 2 w/SIMD)");
   run(chain_kernel<1, 3>, 768, 240, "float  (1 col/lane, 3 w/SIMD)");
   run(chain_kernel<2, 2>, 512, 480, "float2 (2 col/lane, 2 w/SIMD)");
+  {
+    float* dout2;
+    hipMalloc(&dout2, 512 * 512 * 4);
+    auto runf = [&](auto kern, const char* name) {
+      for (int w = 0; w < 3; ++w) kern<<<512, 512>>>(dt, dF, dout2, reps, 0x1fffffu);
+      hipEventRecord(e0);
+      for (int it = 0; it < 10; ++it) kern<<<512, 512>>>(dt, dF, dout2, reps, 0x1fffffu);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      printf("%-28s %.3f ms per launch (512 blocks x 8 waves, l <= 20)\n", name, ms / 10);
+    };
+    runf(fwd_kernel<false>, "fwd scalar");
+    runf(fwd_kernel<true>, "fwd pairs (s,-s)");
+    runf(fwd_kernel<false>, "fwd scalar");
+    runf(fwd_kernel<true>, "fwd pairs (s,-s)");
+  }
   // pair layout vs one column per lane: same operations, bitwise equal sums
   std::vector<float> o1(512 * 256), o2(512 * 256);
   chain_kernel<1, 2><<<512, 256>>>(dt, dF, dtile, dout, 3, 0x7feu);
