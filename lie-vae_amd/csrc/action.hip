@@ -237,6 +237,71 @@ __global__ __launch_bounds__(256) void action_bwd_reduce5_kernel(const float* ws
   }
 }
 
+// The persistent backward's fused tail in one launch: blocks [0, nvjp) run the exp -> ZYZ
+// VJP (exp_eazyz_vjp_sample, one sample per thread: the same per-sample function as
+// lv_exp_eazyz_vjp, so the same bits), blocks [nvjp, nvjp + chunks) the reduce5 dF sum.
+// Both read only the persistent kernel's outputs, so they run side by side instead of
+// back to back (the VJP is one long dependent chain per sample at one wave per SIMD).
+__global__ __launch_bounds__(256) void action_bwd_reduce5_vjp_kernel(const float* ws_F, float* gF, int64_t MC,
+                                                                     int nslab, int nvjp, const float* mu,
+                                                                     const float* v, const float* gang,
+                                                                     float* gmu, float* gv, int64_t n) {
+  if ((int)blockIdx.x < nvjp) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+      float av[3], g[3], m[9], gm[9], o[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { av[k] = v[i * 3 + k]; g[k] = gang[i * 3 + k]; }
+      if (mu) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = mu[i * 9 + k];
+      }
+      exp_eazyz_vjp_sample(av, mu != nullptr, m, g, gm, o);
+      if (mu) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) gmu[i * 9 + k] = gm[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gv[i * 3 + k] = o[k];
+    }
+    return;
+  }
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ f4 part[4][4];
+  const int chunk = (int)blockIdx.x - nvjp;
+  const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
+  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)chunk * nslab * kSlabChunk) + q;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = bs; b0 < nslab; b0 += 64 * kR5Loads) {
+    f4 vv[kR5Loads];
+#pragma unroll
+    for (int u = 0; u < kR5Loads; ++u) {
+      const int b = b0 + 64 * u;
+      vv[u] = b < nslab ? base[(int64_t)b * 4] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kR5Loads; ++u) acc += vv[u];
+  }
+#pragma unroll
+  for (int mm = 4; mm <= 32; mm <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], mm, 64);
+  }
+  const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  if (lane < 4) part[w][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    f4 r = part[0][q];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) r += part[ww][q];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = (int64_t)chunk * kSlabChunk + 4 * q + k;
+      if (e < MC) gF[e] = r[k];
+    }
+  }
+}
+
 namespace {
 
 template <int... Ls>
@@ -677,7 +742,10 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       b.gx = (int)std::min<int64_t>(groups, fallback ? kBwdMaxBlocksFallback : kBwdMaxBlocks);
       if (kEnvGlobal && sharedF) b.gx = (int)std::min<int64_t>(groups, kBwdMaxBlocks);
       b.lds = lds;
-      b.ws = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk) : 0;
+      // shared spectrum: the dF slabs, then the angle-gradient region of the fused path (its
+      // exp -> ZYZ VJP runs beside the reduce, in action_bwd_reduce5_vjp_kernel)
+      b.ws_gang_off = sharedF ? sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk) : 0;
+      b.ws = sharedF ? b.ws_gang_off + sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1) : 0;
       return true;
     }
   }
@@ -772,6 +840,15 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
     p.a.mu = nullptr;
     if (int e = kBwdRun[L](p)) return e;
     static const int kEnvReduceP = LV_KNOB("LV_BWD_REDUCE", kBwdReduceDefault);
+    static const int kEnvVjpMerge = LV_KNOB("LV_BWD_VJP_MERGE", 1);  // A/B: 0 = separate VJP launch
+    if (kEnvReduceP == 6 && v && kEnvVjpMerge) {
+      // fused path: the VJP blocks and the dF reduce in one launch (side by side)
+      const int nvjp = (int)((n + 255) / 256);
+      hipLaunchKernelGGL(action_bwd_reduce5_vjp_kernel, dim3((unsigned)(nvjp + slab_chunks(MC))), dim3(256), 0,
+                         st, (const float*)workspace, gF, MC, b.gx, nvjp, mu, v, (const float*)p.a.gang, gmu,
+                         gv, n);
+      LV_RETURN_LAUNCH("action_bwd_reduce5_vjp_kernel");
+    }
     if (kEnvReduceP == 6)
       hipLaunchKernelGGL(action_bwd_reduce5_kernel, dim3((unsigned)slab_chunks(MC)), dim3(256), 0, st,
                          (const float*)workspace, gF, MC, b.gx);
@@ -782,8 +859,25 @@ int action_bwd_common(const float* ang, const float* F, int64_t F_batch_stride,
     if (v) return lv_exp_eazyz_vjp(mu, v, p.a.gang, gmu, gv, n, st);
     return LV_OK;
   }
+  // fused path: the tile kernel writes the angle gradient to the workspace and the
+  // exp -> ZYZ VJP runs in the reduce's launch, beside it, instead of on wave 0 of every
+  // block after its chain (A/B LV_BWD_TAIL_VJP = 1): 4,096 samples 17.2 -> 15.3 us per
+  // fused backward, 512: 10.9 -> 9.9 (profiles/r05_tail_vjp_ab.txt)
+  static const int kEnvTailVjp = LV_KNOB("LV_BWD_TAIL_VJP", 0);
+  const bool vjp_beside = v && sharedF && p.a.slab_chunked && kEnvReduce == 6 && !kEnvTailVjp;
+  if (vjp_beside) {
+    p.a.gang = reinterpret_cast<float*>(static_cast<char*>(workspace) + b.ws_gang_off);
+    p.a.v = nullptr;
+    p.a.mu = nullptr;
+  }
   if (int e = kBwdRun[L](p)) return e;
   if (!sharedF) return LV_OK;
+  if (vjp_beside) {
+    const int nvjp = (int)((n + 255) / 256);
+    hipLaunchKernelGGL(action_bwd_reduce5_vjp_kernel, dim3((unsigned)(nvjp + slab_chunks(MC))), dim3(256), 0, st,
+                       (const float*)workspace, gF, MC, b.gx, nvjp, mu, v, (const float*)p.a.gang, gmu, gv, n);
+    LV_RETURN_LAUNCH("action_bwd_reduce5_vjp_kernel");
+  }
   // dF slab reduce: chunk-major slabs + action_bwd_reduce5_kernel by default (kBwdReduceDefault;
   // reduce3 before it, profiles/r04_bwd_reduce_ab.txt: 16.0 vs 18.0 us per lv_group_action_bwd call at batch
   // 4,096, 187 vs 191 at 65,536, 9.9 vs 9.8 at 512 against reduce2<16>, the round-3

@@ -589,7 +589,7 @@ void action_bwd_tile_kernel(ActionBwdArgs a) {
 #pragma unroll
           for (int k = 0; k < 9; ++k) m[k] = vmu[tid * 12 + 3 + k];
         }
-        exp_eazyz_vjp_sample(av, a.mu ? m : nullptr, g, gm, o);
+        exp_eazyz_vjp_sample(av, a.mu != nullptr, m, g, gm, o);
         if (a.mu) {
 #pragma unroll
           for (int k = 0; k < 9; ++k) a.gmu[s * 9 + k] = gm[k];

@@ -118,7 +118,7 @@ __global__ void exp_eazyz_vjp_k(const T* mu, const T* v, const T* ga, T* gmu,
     ld(v + i * 3, a);
     ld(ga + i * 3, g);
     if (mu) ld(mu + i * 9, m);
-    exp_eazyz_vjp_sample(a, mu ? m : nullptr, g, gm, o);
+    exp_eazyz_vjp_sample(a, mu != nullptr, m, g, gm, o);
     if (mu) st(gmu + i * 9, gm);
     st(gv + i * 3, o);
   }

@@ -43,20 +43,36 @@ __device__ __forceinline__ T norm3(const T v[3]) {
   return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
 }
 
+// The angle-dependent pieces rodrigues_fwd and rodrigues_bwd both start from, computed
+// once when a caller needs both (exp_eazyz_vjp_sample): the same operations, so the same
+// bits as computing them twice.
 template <typename T>
-__device__ __forceinline__ void rodrigues_fwd(const T v[3], T R[9]) {
-  const T th = norm3(v);
-  const T u[3] = {v[0] / th, v[1] / th, v[2] / th};  // NaN at th == 0, like the reference
-  T K[9], K2[9];
-  hat_sq(u, K, K2);
-  T s, c;
-  lv_sincos(th, &s, &c);
-  const T omc = T(1.) - c;
+struct RodPrep {
+  T th, u[3], K[9], K2[9], s, c;
+};
+template <typename T>
+__device__ __forceinline__ void rodrigues_prep(const T v[3], RodPrep<T>& p) {
+  p.th = norm3(v);
+  p.u[0] = v[0] / p.th;  // NaN at th == 0, like the reference
+  p.u[1] = v[1] / p.th;
+  p.u[2] = v[2] / p.th;
+  hat_sq(p.u, p.K, p.K2);
+  lv_sincos(p.th, &p.s, &p.c);
+}
+template <typename T>
+__device__ __forceinline__ void rodrigues_fwd_p(const RodPrep<T>& p, T R[9]) {
+  const T omc = T(1.) - p.c;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const T eye = (i == 0 || i == 4 || i == 8) ? T(1.) : T(0.);
-    R[i] = (eye + s * K[i]) + omc * K2[i];
+    R[i] = (eye + p.s * p.K[i]) + omc * p.K2[i];
   }
+}
+template <typename T>
+__device__ __forceinline__ void rodrigues_fwd(const T v[3], T R[9]) {
+  RodPrep<T> p;
+  rodrigues_prep(v, p);
+  rodrigues_fwd_p(p, R);
 }
 
 // d/du of <g, s K(u) + w (u u^T - |u|^2 I)>
@@ -86,19 +102,19 @@ __device__ __forceinline__ void polar_vjp(const T v[3], T th, const T gu[3], T g
 }
 
 template <typename T>
-__device__ __forceinline__ void rodrigues_bwd(const T v[3], const T gR[9], T gv[3]) {
-  const T th = norm3(v);
-  const T u[3] = {v[0] / th, v[1] / th, v[2] / th};
-  T K[9], K2[9];
-  hat_sq(u, K, K2);
-  T s, c;
-  lv_sincos(th, &s, &c);
+__device__ __forceinline__ void rodrigues_bwd_p(const T v[3], const RodPrep<T>& p, const T gR[9], T gv[3]) {
   T gth = T(0.);
 #pragma unroll
-  for (int i = 0; i < 9; ++i) gth += gR[i] * (c * K[i] + s * K2[i]);
+  for (int i = 0; i < 9; ++i) gth += gR[i] * (p.c * p.K[i] + p.s * p.K2[i]);
   T gu[3];
-  hat_sq_vjp(u, gR, s, T(1.) - c, gu);
-  polar_vjp(v, th, gu, gth, gv);
+  hat_sq_vjp(p.u, gR, p.s, T(1.) - p.c, gu);
+  polar_vjp(v, p.th, gu, gth, gv);
+}
+template <typename T>
+__device__ __forceinline__ void rodrigues_bwd(const T v[3], const T gR[9], T gv[3]) {
+  RodPrep<T> p;
+  rodrigues_prep(v, p);
+  rodrigues_bwd_p(v, p, gR, gv);
 }
 
 // ------------------------------------------------------------------ 3x3 ops
@@ -171,47 +187,55 @@ __device__ __forceinline__ void mat_to_quat_fwd(const T r[9], T q[4],
   }
 }
 
+// The backward from the forward's own q and case (mat_to_quat_fwd(r, q, &qc) already run).
+// Written without run-time indexing of small arrays (case tables, q[k], den[k]): those put
+// the arrays in scratch memory, a dependent global round trip on the VJP's serial chain.
+// Every gr entry receives exactly one term, 0 + g or 0 - g, so the selects below give the
+// same bits as the per-case accumulation.
+template <typename T>
+__device__ __forceinline__ T sel4(int k, T a0, T a1, T a2, T a3) {
+  return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+}
+template <typename T>
+__device__ __forceinline__ void mat_to_quat_bwd_qc(const T q[4], const QuatCase<T>& qc, const T gq[4], T gr[9]) {
+  const int k = qc.k;
+  const T d = sel4(k, qc.den[0], qc.den[1], qc.den[2], qc.den[3]);
+  const T inv4d = T(1.) / (T(4.) * d);
+  // gradient into the denominator: q_k = d, q_j = N_j / (4 d)
+  T gd = sel4(k, gq[0], gq[1], gq[2], gq[3]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j != k) gd -= gq[j] * q[j] / d;
+  // N_j partials.  Numerators per case: case0 (s01, s02, d12) at q1..q3; case1 (s01, s12,
+  // d20) at q0, q2, q3; case2 (s02, s12, d01) at q0, q1, q3; case3 (d12, d20, d01) at q0..q2;
+  // s01 = r01 + r10, s02 = r02 + r20, s12 = r12 + r21, d12 = r12 - r21, d20 = r20 - r02,
+  // d01 = r01 - r10.
+  T g[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) g[jj] = gq[jj] * inv4d;
+  const T z = T(0.);
+  gr[1] = z + sel4(k, g[1], g[0], g[3], g[2]);                      // s01 | d01
+  gr[3] = k < 2 ? z + sel4(k, g[1], g[0], g[0], g[0]) : z - sel4(k, g[0], g[0], g[3], g[2]);
+  gr[2] = (k == 0 || k == 2) ? z + sel4(k, g[2], g[2], g[0], g[0]) : z - sel4(k, g[3], g[3], g[3], g[1]);
+  gr[6] = z + sel4(k, g[2], g[3], g[0], g[1]);                      // s02 | d20
+  gr[5] = z + sel4(k, g[3], g[2], g[1], g[0]);                      // d12 | s12
+  gr[7] = (k == 1 || k == 2) ? z + sel4(k, g[2], g[2], g[1], g[2]) : z - sel4(k, g[3], g[3], g[3], g[0]);
+  // d = 0.5 sqrt(1e-6 + |pre_k|)
+  const T p = sel4(k, qc.pre[0], qc.pre[1], qc.pre[2], qc.pre[3]);
+  const T t = sqrt(T(1e-6) + fabs(p));
+  const T sg = (p > T(0.)) ? T(1.) : ((p < T(0.)) ? -T(1.) : T(0.));
+  const T gpre = gd * T(0.25) / t * sg;
+  // coef[k][i] = +1 if k == 3 or k == i, else -1
+  gr[0] = z + ((k == 3 || k == 0) ? gpre : -gpre);
+  gr[4] = z + ((k == 3 || k == 1) ? gpre : -gpre);
+  gr[8] = z + ((k == 3 || k == 2) ? gpre : -gpre);
+}
 template <typename T>
 __device__ __forceinline__ void mat_to_quat_bwd(const T r[9], const T gq[4], T gr[9]) {
   T q[4];
   QuatCase<T> qc;
   mat_to_quat_fwd(r, q, &qc);
-  const int k = qc.k;
-  const T d = qc.den[k];
-  const T inv4d = T(1.) / (T(4.) * d);
-#pragma unroll
-  for (int i = 0; i < 9; ++i) gr[i] = T(0.);
-  // gradient into the denominator: q_k = d, q_j = N_j / (4 d)
-  T gd = gq[k];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (j != k) gd -= gq[j] * q[j] / d;
-  // N_j partials: index pairs (p, m, sign of second) for s01, s02, s12, d12, d20, d01
-  auto addN = [&](int which, T g) {
-    switch (which) {
-      case 0: gr[1] += g; gr[3] += g; break;   // s01
-      case 1: gr[2] += g; gr[6] += g; break;   // s02
-      case 2: gr[5] += g; gr[7] += g; break;   // s12
-      case 3: gr[5] += g; gr[7] -= g; break;   // d12 = r12 - r21
-      case 4: gr[6] += g; gr[2] -= g; break;   // d20 = r20 - r02
-      default: gr[1] += g; gr[3] -= g; break;  // d01 = r01 - r10
-    }
-  };
-  // numerators used per case: case0 (s01,s02,d12) at q1..q3; case1 (s01,s12,d20) at q0,q2,q3;
-  // case2 (s02,s12,d01) at q0,q1,q3; case3 (d12,d20,d01) at q0..q2
-  const int tab[4][4] = {{-1, 0, 1, 3}, {0, -1, 2, 4}, {1, 2, -1, 5}, {3, 4, 5, -1}};
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (j != k) addN(tab[k][j], gq[j] * inv4d);
-  // d = 0.5 sqrt(1e-6 + |pre_k|)
-  const T t = sqrt(T(1e-6) + fabs(qc.pre[k]));
-  const T p = qc.pre[k];
-  const T sg = (p > T(0.)) ? T(1.) : ((p < T(0.)) ? -T(1.) : T(0.));
-  const T gpre = gd * T(0.25) / t * sg;
-  const T coef[4][3] = {{T(1.), -T(1.), -T(1.)}, {-T(1.), T(1.), -T(1.)}, {-T(1.), -T(1.), T(1.)}, {T(1.), T(1.), T(1.)}};
-  gr[0] += gpre * coef[k][0];
-  gr[4] += gpre * coef[k][1];
-  gr[8] += gpre * coef[k][2];
+  mat_to_quat_bwd_qc(q, qc, gq, gr);
 }
 
 // ----------------------------------------------------- quaternions_to_eazyz
@@ -294,29 +318,36 @@ __device__ __forceinline__ void quat_to_mat_bwd(const T q0[4], const T g[9], T g
 // the modular kernels lv_so3_exp_fwd + lv_mat_to_eazyz_bwd + lv_so3_exp_bwd (or the
 // so3_sample pair), hence bitwise equal to them.  Shared by lv_exp_eazyz_vjp and the
 // fused backward tile kernel's tail.
+// has_m selects the mu path (a flag, not a nullable pointer: selecting between a local
+// array's address and nullptr forces the array into scratch memory).
 template <typename T>
-__device__ __forceinline__ void exp_eazyz_vjp_sample(const T a[3], const T* m, const T g[3],
+__device__ __forceinline__ void exp_eazyz_vjp_sample(const T a[3], bool has_m, const T m[9], const T g[3],
                                                      T gm[9], T gv[3]) {
+  // the Rodrigues and quaternion intermediates are computed once and shared by the forward
+  // and backward steps (the same operations the modular kernels repeat: same bits)
   T r[9], z[9], q[4], gq[4], gz[9];
-  rodrigues_fwd(a, r);
-  if (m) {
+  RodPrep<T> rp;
+  rodrigues_prep(a, rp);
+  rodrigues_fwd_p(rp, r);
+  if (has_m) {
     matmul3(m, r, z);
   } else {
 #pragma unroll
     for (int k = 0; k < 9; ++k) z[k] = r[k];
   }
-  mat_to_quat_fwd(z, q, nullptr);
+  QuatCase<T> qc;
+  mat_to_quat_fwd(z, q, &qc);
   quat_to_eazyz_bwd(q, g, gq);
-  mat_to_quat_bwd(z, gq, gz);
-  if (m) {
+  mat_to_quat_bwd_qc(q, qc, gq, gz);
+  if (has_m) {
     T t[9], gr[9];
     matmul3_nt(gz, r, t);
 #pragma unroll
     for (int k = 0; k < 9; ++k) gm[k] = T(0) + t[k];
     matmul3_tn(m, gz, gr);
-    rodrigues_bwd(a, gr, gv);
+    rodrigues_bwd_p(a, rp, gr, gv);
   } else {
-    rodrigues_bwd(a, gz, gv);
+    rodrigues_bwd_p(a, rp, gz, gv);
   }
 }
 

@@ -87,8 +87,9 @@ def test_backward_plans_fit_the_kernels(L):
                 assert p["lds_bytes"] <= (LDS_PER_CU if fallback else BWD_MAX_LDS)
                 assert p["blocks"] == min(groups, 1024 if fallback else BWD_MAX_BLOCKS)
                 # workspace: the dF slabs, one per block, sized for the chunk-major layout
-                # (16-element chunks, action_bwd.h kSlabChunk)
-                assert p["aux"] == (4 * p["blocks"] * slab if shared else 0)
+                # (16-element chunks, action_bwd.h kSlabChunk), then the fused path's
+                # angle-gradient region (3 floats per sample)
+                assert p["aux"] == (4 * p["blocks"] * slab + 4 * 3 * n if shared else 0)
                 assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
 
 

@@ -4,6 +4,9 @@ batch, for a rocprofv3 kernel trace that reconciles with bench.py's fwd_bwd.acti
 figure (same call, same capture: 50 calls per graph, replayed).
 
   rocprofv3 --kernel-trace --stats -d gpurun_out/p -o run -- python3 tools/bwd_only.py 4096
+
+Third argument "fused": lv_fused_exp_action_bwd instead (the training path: the same
+kernels plus the exp -> ZYZ VJP, v -> gv, from the forward's saved angles).
 """
 import ctypes
 import json
@@ -19,6 +22,7 @@ sys.path[:0] = [os.path.join(REPO, "lie-vae_amd"), REPO]
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    fused = len(sys.argv) > 3 and sys.argv[3] == "fused"
     L, C = 10, 10
     M = (L + 1) ** 2
     from lie_vae import _lib
@@ -35,10 +39,24 @@ def main():
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     s = torch.cuda.Stream(dev)
 
+    v = (torch.rand(B, 3, generator=g) * 2 - 1).to(dev)
+    gv = torch.empty(B, 3, device=dev)
+    if fused:  # the forward's saved angles for v
+        out = torch.empty(B, (L + 1) ** 2, C, device=dev)
+        rc = lib.lv_fused_exp_action_fwd(None, P(v), P(F), 0, P(out), 0, P(ang), B, L, C, 0,
+                                         ctypes.c_void_p(s.cuda_stream))
+        if rc:
+            raise RuntimeError(_lib.last_error())
+        torch.cuda.synchronize(dev)
+
     def call(k):
         for _ in range(k):
-            rc = lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0,
-                                         P(ws), ws_bytes, ctypes.c_void_p(s.cuda_stream))
+            if fused:
+                rc = lib.lv_fused_exp_action_bwd(None, P(v), P(ang), P(F), P(gout), None, P(gv), P(gF),
+                                                 B, L, C, 0, P(ws), ws_bytes, ctypes.c_void_p(s.cuda_stream))
+            else:
+                rc = lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0,
+                                             P(ws), ws_bytes, ctypes.c_void_p(s.cuda_stream))
             if rc:
                 raise RuntimeError(_lib.last_error())
 
@@ -62,7 +80,7 @@ def main():
     import numpy as np
     gf = gF.cpu().numpy()
     np.save(os.path.join(REPO, "gpurun_out", f"bwd_only_gF_{B}_{os.environ.get('LV_BWD_VARIANT', 'd')}.npy"), gf)
-    print(json.dumps({"batch": B, "calls": reps * 50, "us_per_call": us,
+    print(json.dumps({"batch": B, "fused": fused, "calls": reps * 50, "us_per_call": us,
                       "gF_sha": hashlib.sha1(gf.tobytes()).hexdigest()[:12],
                       "gang_sha": hashlib.sha1(gang.cpu().numpy().tobytes()).hexdigest()[:12],
                       "plan": _lib.plan("bwd", B, L, C, 1)}), flush=True)
