@@ -529,11 +529,11 @@ def test_exp_eazyz_vjp_matches_modular_bitwise(gpu_device):
 
 
 def test_fused_exp_action_bwd_matches_modular_bitwise(gpu_device):
-    """lv_fused_exp_action_bwd (group-action backward with the exp -> ZYZ VJP in the tile
-    kernel's tail, the angle gradient never leaving the chip) against lv_group_action_bwd
-    + lv_exp_eazyz_vjp, bit for bit: with and without a mean, transposed, ragged batches
-    and the grid-capped looped path (more groups than blocks), in the LDS and the large-tile
-    spectrum modes."""
+    """lv_fused_exp_action_bwd (group-action backward with the exp -> ZYZ VJP in the dF
+    reduce's launch, action_bwd_reduce5_vjp_kernel, for the one-group and the persistent
+    tile kernels) against lv_group_action_bwd + lv_exp_eazyz_vjp, bit for bit: with and
+    without a mean, transposed, ragged batches, the persistent kernel (20,003 samples) and
+    the large-tile spectrum mode."""
     import lie_vae._lib as lib
     from lie_vae._lib import call, ptr, stream
     import lie_vae.lie_tools as lt
