@@ -167,8 +167,9 @@ int lv_group_action_bwd(const float* ang, const float* F, int64_t F_batch_stride
 int lv_fused_exp_action_fwd(const float* mu, const float* v, const float* F,
                             int64_t F_batch_stride, void* out, int out_dtype, float* ang_out,
                             int64_t n, int L, int C, int transpose, void* stream);
-/* Its backward in one pass (shared spectrum): the group-action backward with the angle
- * gradient kept on chip and the exp -> ZYZ VJP applied per sample in the same kernel;
+/* Its backward in two launches (shared spectrum): the group-action backward writes the
+ * angle gradient to the workspace, and the exp -> ZYZ VJP runs per sample in the dF
+ * reduce's launch, beside the reduce;
  * gmu (n,3,3, when mu is given), gv (n,3), gF (M,C).  Bitwise equal to
  * lv_group_action_bwd + lv_exp_eazyz_vjp.  ang = the forward's ang_out; workspace as
  * lv_group_action_bwd_workspace(n, L, C, 1). */

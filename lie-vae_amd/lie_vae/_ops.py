@@ -302,7 +302,8 @@ def _f32c(t):
 
 class _FusedExpAction(torch.autograd.Function):
     """mu@exp(v) -> ZYZ -> block D·F in one launch; backward = one tile-kernel launch
-    (group-action backward with the exp -> ZYZ VJP in its tail) + the dF slab reduce.
+    (group-action backward) + one launch of the dF slab reduce with the exp -> ZYZ VJP
+    beside it.
     Host path kept short (the eager training direction is host-bound at config 2): no
     conversion calls on already-fp32 contiguous inputs, the workspace cached per stream."""
 
