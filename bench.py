@@ -662,6 +662,7 @@ def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     torch.cuda.synchronize(dev)
     tg = e0.elapsed_time(e1) / 1e3 / reps
     kern = bench_action_bwd_kernel(vg.detach(), F, gout, L, dev)
+    kern_fused = bench_action_bwd_kernel(vg.detach(), F, gout, L, dev, fused=True)
     # the large-batch backward (persistent kernel, action_bwd_persist.h) at 65,536 samples
     g2 = torch.Generator(device="cpu").manual_seed(77)
     vb = torch.randn(65536, 3, generator=g2).to(dev)
@@ -671,16 +672,18 @@ def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     return {"value": B / tg, "unit": "samples/s", "us_per_step": tg * 1e6,
             "launch": "graph (forward + backward captured once, replayed)",
             "eager_us_per_step": t * 1e6, "eager_value": B / t,
-            "action_bwd": kern,
+            "action_bwd": kern, "action_bwd_fused": kern_fused,
             "action_bwd_65536": kern_big,
             "note": "one training-direction pass: fused forward, group-action backward "
                     "kernel + deterministic dF reduce + fused exp/ZYZ VJP"}
 
 
-def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):
+def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200, fused=False):
     """lv_group_action_bwd alone (backward tile kernel + deterministic dF reduce), graph-
     captured back-to-back calls on resident inputs: the angle/spectrum gradient of
-    block_wigner_matrix_multiply (lie_tools.py:226-253) at the metric size."""
+    block_wigner_matrix_multiply (lie_tools.py:226-253) at the metric size.  fused=True:
+    lv_fused_exp_action_bwd, the training path (the same kernels, the exp -> ZYZ VJP beside
+    the reduce; v -> gv instead of the angle gradient)."""
     import lie_vae._ops as ops
     from lie_vae import _lib
     lib = _lib.load()
@@ -692,6 +695,7 @@ def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):
                                 ctypes.c_void_p(out.data_ptr()), _lib.LV_DTYPE_F32,
                                 ctypes.c_void_p(ang.data_ptr()), B, L, C, 0, None)
     gang = torch.empty(B, 3, device=dev)
+    gv = torch.empty(B, 3, device=dev)
     gF = torch.empty(M, C, device=dev)
     ws_bytes = lib.lv_group_action_bwd_workspace(B, L, C, 1)
     ws = torch.empty(max(ws_bytes, 1), device=dev, dtype=torch.uint8)
@@ -701,8 +705,12 @@ def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):
 
     def call(k, st):
         for _ in range(k):
-            rc = lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0,
-                                         P(ws), ws_bytes, ctypes.c_void_p(st.cuda_stream))
+            if fused:
+                rc = lib.lv_fused_exp_action_bwd(None, P(v), P(ang), P(F), P(gout), None, P(gv), P(gF),
+                                                 B, L, C, 0, P(ws), ws_bytes, ctypes.c_void_p(st.cuda_stream))
+            else:
+                rc = lib.lv_group_action_bwd(P(ang), P(F), 0, P(gout), P(gang), P(gF), B, L, C, 0,
+                                             P(ws), ws_bytes, ctypes.c_void_p(st.cuda_stream))
             if rc:
                 raise RuntimeError(_lib.last_error())
 
@@ -728,8 +736,9 @@ def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200):
     return {"us_per_call": us, "batch": B, "samples_per_s": B / us * 1e6, "bytes_per_call": bb,
             "achieved_GBs": bb / us / 1e3, "frac": bb / us / 1e3 / HBM_PEAK_GBS,
             "min_bytes_per_call": bmin, "frac_min_bytes": bmin / us / 1e3 / HBM_PEAK_GBS,
-            "kernel": "persistent (action_bwd_persist_kernel)" if plan["tile"] == 3 else
-                      "one group per block (action_bwd_tile_kernel)",
+            "kernel": ("persistent (action_bwd_persist_kernel)" if plan["tile"] == 3 else
+                       "one group per block (action_bwd_tile_kernel)") +
+                      (" + reduce5 with the exp -> ZYZ VJP beside it (lv_fused_exp_action_bwd)" if fused else ""),
             "blocks": plan["blocks"],
             "bytes_note": "angles + output gradient in, angle gradient out, F in / dF out, "
                           "the dF slabs written and read once (one per block); "
