@@ -667,7 +667,7 @@ def bench_fwd_bwd(v, F, L, dev, stream, iters=200):
     g2 = torch.Generator(device="cpu").manual_seed(77)
     vb = torch.randn(65536, 3, generator=g2).to(dev)
     gb = torch.randn(65536, (L + 1) ** 2, C, generator=g2).to(dev)
-    kern_big = bench_action_bwd_kernel(vb, F, gb, L, dev, reps=100)
+    kern_big = bench_action_bwd_kernel(vb, F, gb, L, dev, reps=200)
     del vb, gb
     return {"value": B / tg, "unit": "samples/s", "us_per_step": tg * 1e6,
             "launch": "graph (forward + backward captured once, replayed)",
