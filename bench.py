@@ -43,6 +43,17 @@ from lie_vae.experiments import launch  # noqa: E402  (imports torch only; no HI
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 via v_pk_fma_f32 (= fp32 MFMA)
+# The group-action backward is VALU-issue bound at large batch, so its records carry a VALU
+# roofline next to the HBM one: the kernel's VALU wave-instructions per call (PMC
+# SQ_INSTS_VALU of the backward kernel + its dF reduce, measured at HEAD with
+# tools/gpu_pmc_bwd_only.sh) at the chip's measured scalar-FMA issue rate (661.19 wave
+# instructions per ns = 3.72 cycles per instruction per SIMD, 8 waves per SIMD,
+# tools/valu_rate.hip, profiles/r05_valu_rate.txt), as a fraction of the call time.
+VALU_WAVE_INSTS_PER_NS = 661.19
+BWD_VALU_PER_CALL = {  # batch -> (SQ_INSTS_VALU per call, evidence)
+    4096: (3149306 + 51604, "profiles/r06_pmc_bwd_only_4096.txt"),
+    65536: (50138643 + 84056, "profiles/r05_pmc_persist_65536.txt"),
+}
 SCRUB_BYTES = 512 << 20  # > 256 MiB Infinity Cache (MI355X_MICROARCH.md:40)
 
 
@@ -733,7 +744,14 @@ def bench_action_bwd_kernel(v, F, gout, L, dev, reps=200, fused=False):
     slab_bytes = plan["blocks"] * (-(-M * C // 16) * 16) * 4
     bb = B * (12 + M * C * 4 + 12) + 2 * M * C * 4 + slab_bytes * 2
     bmin = B * (12 + M * C * 4 + 12) + 2 * M * C * 4
-    return {"us_per_call": us, "batch": B, "samples_per_s": B / us * 1e6, "bytes_per_call": bb,
+    valu = None
+    if not fused and B in BWD_VALU_PER_CALL:
+        insts, src = BWD_VALU_PER_CALL[B]
+        issue_us = insts / VALU_WAVE_INSTS_PER_NS / 1e3
+        valu = {"bound": "valu", "valu_wave_insts_per_call": insts, "issue_us": issue_us,
+                "rate_wave_insts_per_ns": VALU_WAVE_INSTS_PER_NS, "frac": issue_us / us,
+                "source": src + " (PMC) / profiles/r05_valu_rate.txt (issue rate)"}
+    return {"us_per_call": us, "roofline_valu": valu, "batch": B, "samples_per_s": B / us * 1e6, "bytes_per_call": bb,
             "achieved_GBs": bb / us / 1e3, "frac": bb / us / 1e3 / HBM_PEAK_GBS,
             "min_bytes_per_call": bmin, "frac_min_bytes": bmin / us / 1e3 / HBM_PEAK_GBS,
             "kernel": ("persistent (action_bwd_persist_kernel)" if plan["tile"] == 3 else

@@ -139,13 +139,28 @@ int lv_group_action_fwd(const float* ang, const float* F, int64_t F_batch_stride
 
 /* Backward of lv_group_action_fwd (fp32 gout).  gang (n,3).  gF is (M,C) summed
  * over the batch (deterministic two-stage reduction through the workspace) when
- * F_batch_stride == 0, else (n,M,C).  Workspace bytes from the query below. */
+ * F_batch_stride == 0, else (n,M,C).  Workspace bytes from the query below.
+ * ABI note (version 2 of the workspace contract, round 5): with a shared spectrum the
+ * workspace holds the dF slabs AND a 12-byte-per-sample angle-gradient region that only
+ * lv_fused_exp_action_bwd writes; both entry points take the same query, so a caller that
+ * cached an older (slabs-only) size gets LV_ERR_WORKSPACE -- re-query per (n, L, C).
+ * The slab count follows the device's CU count (lv_compute_units), so query on the device
+ * the call runs on. */
 size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F);
 
-/* Launch plans (host only, no GPU call; for tests and capacity planning).  plan[] gets
+/* Compute units of the current HIP device (hipDeviceAttributeMultiprocessorCount, cached
+ * per device; 256, the MI355X count, when no device is visible): the persistent
+ * backward's grid is 3 blocks per CU, so its plan, workspace and dF summation order
+ * follow the part (a CPX partition has fewer CUs). */
+int lv_compute_units(void);
+
+/* Launch plans (host only, no kernel launch; for tests and capacity planning; the backward
+ * reads the device's CU count as lv_compute_units does).  plan[] gets
  * LV_PLAN_LEN values: [0] forward: tile kernel (1) or grid-stride kernel (0); backward:
  * spectrum mode (0 per-sample, 1 shared in LDS, 2 shared from global memory with the dF
- * slab in the workspace -- the large-tile fallback), [1] grid blocks,
+ * slab in the workspace -- the large-tile fallback, 3 the persistent kernel: C = 10,
+ * 3 <= l <= 10, shared spectrum, from 3 * CUs + 1 six-sample groups (769 on MI355X),
+ * 3 blocks per CU, one dF slab per block), [1] grid blocks,
  * [2] degree segments, [3] threads per block, [4] dynamic LDS bytes per block,
  * [5] samples per block group, [6] forward: write-through stores / backward: workspace
  * bytes, [7..23] segment boundaries seg_lo[0..segments] (then -1), [24..39] the degree

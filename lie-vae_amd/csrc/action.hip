@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <array>
+#include <atomic>
 #include <vector>
 
 #include "action_kernels.h"
@@ -201,11 +202,14 @@ __global__ __launch_bounds__(1024) void action_bwd_reduce4_kernel(const float* w
 // order after one barrier.  Fewer threads and barriers than reduce3 (1,024 threads, an
 // 8-level tree); deterministic in a fixed order of its own.
 constexpr int kR5Loads = 12;
-__global__ __launch_bounds__(256) void action_bwd_reduce5_kernel(const float* ws_F, float* gF, int64_t MC, int nslab) {
+// The reduce5 body for one chunk: the modular reduce and the fused VJP launch's reduce blocks
+// both call it, so their dF is the same fixed summation order by construction (the bitwise
+// fused-vs-modular contract).
+__device__ __forceinline__ void reduce5_chunk(const float* ws_F, float* gF, int64_t MC, int nslab, int chunk) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   __shared__ f4 part[4][4];
   const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
-  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)blockIdx.x * nslab * kSlabChunk) + q;
+  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)chunk * nslab * kSlabChunk) + q;
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int b0 = bs; b0 < nslab; b0 += 64 * kR5Loads) {
     f4 v[kR5Loads];
@@ -231,10 +235,13 @@ __global__ __launch_bounds__(256) void action_bwd_reduce5_kernel(const float* ws
     for (int ww = 1; ww < 4; ++ww) r += part[ww][q];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int64_t e = (int64_t)blockIdx.x * kSlabChunk + 4 * q + k;
+      const int64_t e = (int64_t)chunk * kSlabChunk + 4 * q + k;
       if (e < MC) gF[e] = r[k];
     }
   }
+}
+__global__ __launch_bounds__(256) void action_bwd_reduce5_kernel(const float* ws_F, float* gF, int64_t MC, int nslab) {
+  reduce5_chunk(ws_F, gF, MC, nslab, (int)blockIdx.x);
 }
 
 // The persistent backward's fused tail in one launch: blocks [0, nvjp) run the exp -> ZYZ
@@ -266,40 +273,7 @@ __global__ __launch_bounds__(256) void action_bwd_reduce5_vjp_kernel(const float
     }
     return;
   }
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  __shared__ f4 part[4][4];
-  const int chunk = (int)blockIdx.x - nvjp;
-  const int q = (int)threadIdx.x & 3, bs = (int)threadIdx.x >> 2;
-  const f4* base = reinterpret_cast<const f4*>(ws_F + (int64_t)chunk * nslab * kSlabChunk) + q;
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int b0 = bs; b0 < nslab; b0 += 64 * kR5Loads) {
-    f4 vv[kR5Loads];
-#pragma unroll
-    for (int u = 0; u < kR5Loads; ++u) {
-      const int b = b0 + 64 * u;
-      vv[u] = b < nslab ? base[(int64_t)b * 4] : f4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int u = 0; u < kR5Loads; ++u) acc += vv[u];
-  }
-#pragma unroll
-  for (int mm = 4; mm <= 32; mm <<= 1) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], mm, 64);
-  }
-  const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-  if (lane < 4) part[w][lane] = acc;
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    f4 r = part[0][q];
-#pragma unroll
-    for (int ww = 1; ww < 4; ++ww) r += part[ww][q];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t e = (int64_t)chunk * kSlabChunk + 4 * q + k;
-      if (e < MC) gF[e] = r[k];
-    }
-  }
+  reduce5_chunk(ws_F, gF, MC, nslab, (int)blockIdx.x - nvjp);
 }
 
 namespace {
@@ -634,7 +608,27 @@ constexpr double kBwdSegCost = 2.2 * 1000.0;
 // segments at l = 10 (2 / 3 / 4 / 6 / 8 ran 24.2 / 22.2 / 19.5 / 27.8 / 26.9 us per call,
 // profiles/r02_bwd_regbudget_sweep.txt).
 constexpr double kBwdSegCostWide = 1.1 * 1000.0;
-constexpr int64_t kBwdCUs = 256;  // MI355X compute units
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount, cached per
+// device): the persistent backward's grid (3 blocks per CU), and with it the dF summation
+// order, follows the part it runs on -- 256 on a full MI355X, fewer on a CPX partition.
+// Without a device (CPU-only host planning) the MI355X count.
+constexpr int kDefaultCUs = 256;
+int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return kDefaultCUs;
+  }
+  static std::atomic<int> cache[64];
+  int cus = cache[dev].load(std::memory_order_relaxed);
+  if (cus > 0) return cus;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+    (void)hipGetLastError();
+    cus = kDefaultCUs;
+  }
+  cache[dev].store(cus, std::memory_order_relaxed);
+  return cus;
+}
 // LV_BWD_REDUCE default (see action_bwd_common): 6 = chunk-major slabs + reduce5 (one
 // 256-thread block per 16-element chunk).  Same box, backward alone (profiles/r05_reduce_ab.txt):
 // 512: 8.93 -> 8.72 us, 4,096: 14.45 -> 13.94, 16,384: 32.2 -> 31.9, 65,536: 103.4 -> 102.5
@@ -664,33 +658,33 @@ struct BwdPlan {
   size_t lds, ws;
 };
 
-// Persistent backward (action_bwd_persist.h) from this many 6-sample groups up, i.e. once
-// the batch needs more than one round of 3 blocks per CU: 3 blocks per CU walk the groups,
-// the next group's multiples prefetched, one dF slab per block.  Below it the one-group
-// kernel (one round of blocks, the fused VJP in its tail) is shorter (4,096: 14.26 vs
-// 14.47 us; 9,216: 24.9 vs 23.1; 16,384: 38.8 vs 33.5; 65,536: 182 vs 110,
-// profiles/r05_bwd_persist_ab2.txt).
-constexpr int64_t kBwdPersistMinGroups = 769;
+// Persistent backward (action_bwd_persist.h) once the batch needs more than one round of 3
+// blocks per CU (more than 3 * CUs 6-sample groups: 769 on MI355X): 3 blocks per CU walk
+// the groups, the next group's multiples prefetched, one dF slab per block.  Below it the
+// one-group kernel (one round of blocks) is shorter (4,096: 14.26 vs 14.47 us; 9,216: 24.9
+// vs 23.1; 16,384: 38.8 vs 33.5; 65,536: 182 vs 110, profiles/r05_bwd_persist_ab2.txt).
 
-bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
+bool plan_bwd(int64_t n, int L, int C, bool sharedF, int cus, BwdPlan& b) {
   static const int kEnvNseg = LV_KNOB("LV_BWD_NSEG", 0);      // A/B testing only
   static const int kEnvGlobal = LV_KNOB("LV_BWD_FGLOBAL", 0);  // force the fallback (tests)
-  static const int kEnvPersistMin = LV_KNOB("LV_BWD_PERSIST_MIN", (int)kBwdPersistMinGroups);  // A/B; 0 = off
+  static const int kEnvPersistMin = LV_KNOB("LV_BWD_PERSIST_MIN", -1);  // A/B; 0 = off, -1 = 3 * CUs + 1
+  static const int kEnvVariantP = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
+  const bool single = (kEnvVariantP & kBwdVarPersistSingle) != 0;  // A/B: one tile buffer
+  const int64_t persist_blocks = (int64_t)cus * (single ? kBwdPersistBlocksPerCU : kBwdPersistBlocksPerCUDB);
+  const int64_t persist_min = kEnvPersistMin < 0 ? (int64_t)cus * kBwdPersistBlocksPerCU + 1 : kEnvPersistMin;
   b = BwdPlan{};
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
   if (sharedF && C == kTileFastC && L >= kBwdPersistWaves - 1 && L <= kBwdPersistMaxL && !kEnvGlobal &&
-      kEnvPersistMin > 0) {
+      persist_min > 0) {
     const int Sw = 64 / C;
     const int64_t groups = (std::max<int64_t>(n, 1) + Sw - 1) / Sw;
-    if (groups >= kEnvPersistMin) {
+    if (groups >= persist_min) {
       b.persist = 1;
       b.Sw = Sw;
       b.nseg = kBwdPersistWaves;
       b.fmode = kBwdFShared;
       b.groups = groups;
-      static const int kEnvVariantP = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
-      const bool single = (kEnvVariantP & kBwdVarPersistSingle) != 0;  // A/B: one tile buffer
-      b.gx = (int)std::min<int64_t>(groups, kBwdCUs * (single ? 3 : kBwdPersistBlocksPerCU));
+      b.gx = (int)std::min<int64_t>(groups, persist_blocks);
       plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
       balance_masks(L, b.nseg, true, b.seg_mask);
       b.lds = sizeof(float) * (size_t)persist_lds_floats(L, b.nseg, single ? 1 : 2);
@@ -713,7 +707,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
       // small batches: at most one group per CU leaves wave slots free, so the chain is
       // split into 8 segments (l = 10: batch 512 4 / 6 / 8 segments 11.9 / 10.5 / 10.3 us;
       // at 2,048 (342 groups) 6 and 8 segments were slower than 4: 19.3 / 18.6 vs 14.9)
-      if (bwd_wide(L, C, fmode, groups, gx) && groups <= kBwdCUs) nseg = std::max(nseg, std::min(8, L + 1));
+      if (bwd_wide(L, C, fmode, groups, gx) && groups <= cus) nseg = std::max(nseg, std::min(8, L + 1));
       if (kEnvNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvNseg);
       nseg = std::min(L + 1, std::max(nseg, (3 * Sw + 63) / 64));
       if (3 * Sw > 64 * nseg || nseg > 8) continue;
@@ -752,16 +746,17 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   return false;
 }
 
-using BwdKey = std::array<int64_t, 4>;  // n, L, C, shared spectrum
+using BwdKey = std::array<int64_t, 5>;  // n, L, C, shared spectrum, device CUs
 
 bool plan_bwd_cached(int64_t n, int L, int C, bool sharedF, BwdPlan& b) {
   thread_local PlanCache<BwdKey, BwdPlan> cache;
-  const BwdKey k{n, L, C, sharedF ? 1 : 0};
+  const int cus = device_cus();
+  const BwdKey k{n, L, C, sharedF ? 1 : 0, cus};
   if (const BwdPlan* hit = cache.find(k)) {
     b = *hit;
     return true;
   }
-  if (!plan_bwd(n, L, C, sharedF, b)) return false;
+  if (!plan_bwd(n, L, C, sharedF, cus, b)) return false;
   cache.put(k, b);
   return true;
 }
@@ -995,7 +990,7 @@ int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* pla
   LV_CHECK_ARG(n > 0, "n must be > 0 (got %lld)", (long long)n);
   if (int e = check_common(n, L, C, LV_DTYPE_F32)) return e;
   BwdPlan b;
-  LV_CHECK_ARG(plan_bwd(n, L, C, shared_F != 0, b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
+  LV_CHECK_ARG(plan_bwd(n, L, C, shared_F != 0, device_cus(), b), "no backward plan fits the LDS budget (l=%d, C=%d)", L, C);
   plan[0] = b.persist ? 3 : b.fmode;
   plan[1] = b.gx;
   plan[2] = b.nseg;
@@ -1007,6 +1002,8 @@ int lv_group_action_bwd_plan(int64_t n, int L, int C, int shared_F, int64_t* pla
   for (int k = 0; k < kMaxSeg; ++k) plan[8 + kMaxSeg + k] = k < b.nseg ? (int64_t)b.seg_mask[k] : 0;
   return LV_OK;
 }
+
+int lv_compute_units(void) { return device_cus(); }
 
 int lv_wigner_d_fwd(const float* ang, float* D, int64_t n, int L, void* stream) {
   clear_error();

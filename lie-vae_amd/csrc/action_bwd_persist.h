@@ -26,14 +26,16 @@
 // operation.  Summation orders are fixed by the plan (degree set per wave, groups per
 // block): reproducible bit for bit, and within fp32 rounding of the one-group kernel.
 // The angle gradient goes to a.gang (the caller's, or a workspace region for the fused
-// exp -> ZYZ VJP, which the host then runs as lv_exp_eazyz_vjp's kernel).
+// exp -> ZYZ VJP, which the host then runs beside the dF reduce, in
+// action_bwd_reduce5_vjp_kernel).
 // Included by action_bwd.h after the one-group kernel and its helpers.
 
 namespace lv {
 
 constexpr int kBwdPersistMaxL = 10;
 constexpr int kBwdPersistWaves = 4;      // degree-set waves per block
-constexpr int kBwdPersistBlocksPerCU = 2;
+constexpr int kBwdPersistBlocksPerCU = 3;    // one gradient-tile buffer (the product)
+constexpr int kBwdPersistBlocksPerCUDB = 2;  // double-buffered tile (A/B)
 // A/B variant bits of the persistent kernel (ActionBwdArgs::variant, A/B build only):
 // single gradient-tile buffer at 3 blocks per CU (3 waves per SIMD; the next tile is
 // loaded after the group's barrier); the next group's multiples filled by the 18 first lanes

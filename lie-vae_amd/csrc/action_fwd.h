@@ -358,8 +358,9 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     float cq, sq;
     if constexpr (FUSED && !MAYMU) {
       // z = exp(v): this thread's slot only (transpose: slot q takes angle 2 - q, sine negated)
-      // ang_out is written after the chain by the last wave (below): its atan2 / acos
-      // chain kept the multiples waiting on the q = 0 lanes
+      // ang_out is not written here: wave 1 writes it during the prologue (above; a one-wave
+      // block after its chain), since its atan2 / acos kept the multiples waiting on the
+      // q = 0 lanes
       float qr[4];
       exp_to_zyz_slot(in.v, a.transpose ? 2 - q : q, cq, sq, qr);
       if (a.transpose) sq = -sq;

@@ -26,6 +26,7 @@ _F = ctypes.c_float
 _SIGS = {
     "lv_abi_version": [],
     "lv_max_degree": [],
+    "lv_compute_units": [],
     "lv_so3_exp_fwd": [_P, _P, _I64, _P],
     "lv_so3_exp_bwd": [_P, _P, _P, _I64, _P],
     "lv_so3_sample_fwd": [_P, _P, _P, _I64, _I64, _P],

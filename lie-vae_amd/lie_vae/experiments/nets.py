@@ -32,7 +32,10 @@ def use_packaged_miopen_db():
     the recorded winners instead of its fallback heuristics, which pick ConvDirectNaive
     kernels (30-300 ms per call) for several NHWC bf16 shapes.  Must run before the
     process's first convolution; a MIOPEN_USER_DB_PATH already set is left alone.  Returns
-    the directory in use (None if the package has no db)."""
+    the directory in use (None if the package has no db).  The private copy is removed at
+    interpreter exit (atexit), so repeated runs and DP ranks leave nothing in the temp
+    directory."""
+    import atexit
     import os
     import shutil
     import tempfile
@@ -42,6 +45,7 @@ def use_packaged_miopen_db():
     if not os.path.isdir(src):
         return None
     dst = tempfile.mkdtemp(prefix="lievae_miopen_db_")
+    atexit.register(shutil.rmtree, dst, True)
     for f in os.listdir(src):
         shutil.copy(os.path.join(src, f), dst)
     os.environ["MIOPEN_USER_DB_PATH"] = dst

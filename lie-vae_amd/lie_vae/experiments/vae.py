@@ -20,6 +20,17 @@ from .nets import MLP, ConvNet, ConvNetBN, DeconvNet, Flatten
 
 _MEANS = {'alg': AlgebraMean, 'q': QuaternionMean, 's2s1': S2S1Mean, 's2s2': S2S2Mean}
 
+# Under reduced-precision autocast, the latent heads -- the encoder's last (4x4 -> 1x1)
+# GEMM conv and the mean / sigma linears (reparameterize.py:148-197) -- compute in fp32:
+# 0 = off (all autocast), 1 = the rep_group heads, 2 = the heads and the encoder's last
+# conv.  A bf16 rounding of the mean map's output is a 2^-9 perturbation of the S2S2
+# Gram-Schmidt's input, whose near-parallel pairs amplify it; the layers
+# are (512 x 6400) x (6400 x 10) and (10 x 6) GEMMs, so fp32 costs nothing measurable.
+# Over 50 config-3 steps (s2s2) the bf16 trajectory's distance from the fp32 one
+# (rep_group: cos -0.15 / 0.75 / 0.66 for modes 0 / 1 / 2, against 0.30 for fp32 itself
+# under a 2^-9 input perturbation; profiles/r06_bf16_trajectory_s2s2.json): mode 1.
+AMP_FP32_HEADS = 1
+
 
 class VAE(nn.Module):
     def __init__(self, *, latent_mode, decoder_mode, degrees=6, deconv_hidden=50,
@@ -88,7 +99,24 @@ class VAE(nn.Module):
             raise RuntimeError()
 
     def encode(self, x, n=1, eps=None):
-        h = self.encoder(x)
+        amp = torch.is_autocast_enabled(x.device.type) and AMP_FP32_HEADS > 0
+        if amp and AMP_FP32_HEADS > 1 and isinstance(self.encoder, nn.Sequential):
+            mods = list(self.encoder)
+            h = x
+            for m in mods[:-2]:
+                h = m(h)
+            with torch.autocast(x.device.type, enabled=False):
+                h = h.float()
+                for m in mods[-2:]:
+                    h = m(h)
+        else:
+            h = self.encoder(x)
+        if amp:
+            with torch.autocast(x.device.type, enabled=False):
+                return self._reparam(h.float(), n, eps)
+        return self._reparam(h, n, eps)
+
+    def _reparam(self, h, n, eps):
         if self.r_callback is not None:
             return [r(f(h), n) for r, f in zip(self.reparameterize, self.r_callback)]
         if eps is not None:

@@ -15,6 +15,14 @@ for p in (PKG_ROOT, REPO):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    # MIOpen immediate mode off the find-db shipped with the package, as bench.py and
+    # bench_train.py run it (before any convolution in this process); without it some NHWC
+    # bf16 shapes take MIOpen's naive fallback kernels (~1.5 s per config-3 step)
+    try:
+        from lie_vae.experiments import nets
+        nets.use_packaged_miopen_db()
+    except ImportError:
+        pass
 
 
 def golden(name):

@@ -151,7 +151,9 @@ def test_out_dtype_validated_before_any_path():
             _ops.group_action(torch.randn(4, 3), F, 3, out_dtype=dt)
 
 
-def test_require_device_refuses_cpu_and_mixed():
+def test_require_device_refuses_cpu():
+    """The CPU case (no device here); the mixed-device case is a GPU test
+    (test_gpu_parity.py::test_torch_operator_refuses_cpu_or_mixed_inputs)."""
     from lie_vae import _lib
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.require_device(None, torch.randn(2))

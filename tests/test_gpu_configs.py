@@ -316,16 +316,12 @@ def test_dp_trainer_bf16_autocast_step(gpu_device):
 BF16_STEP_TOL = 0.06
 BF16_STEP_K = 16.0
 BF16_KAPPA_MAX = 0.01
-# Groups whose fp32 gradient is itself ill-conditioned at this initialisation, so that the
-# bound is allowed to come from the 16·kappa branch with kappa > BF16_KAPPA_MAX (DESIGN.md
-# §2 "bf16 step conditioning", profiles/r05_bf16_step_cond.json): a 2^-9 input
-# perturbation of the FP32 step moves item_rep's gradient by 7.5% in every mean mode (the
-# l = 10 Wigner blocks turn a ~1e-3 rad change of the latent rotation into percent-level
-# changes of D), rep_group's by 5% and the encoder's by 116% (s2s2: the Gram-Schmidt of
-# nearly parallel (v1, v2) pairs, mapped with U(-10, 10) weights, reparameterize.py:190-192;
-# 46% with the 16 worst-conditioned samples masked, 9% with mean_mode alg).  The deconv
-# stack is well conditioned (kappa 1.2e-4) and held to BF16_STEP_TOL.
-BF16_KAPPA_JUSTIFIED = {"encoder", "rep_group", "item_rep"}
+# Groups whose fp32 gradient is itself ill-conditioned at this initialisation (kappa >
+# BF16_KAPPA_MAX: encoder 1.16, rep_group 0.053, item_rep 0.075 -- DESIGN.md §2 "bf16 step
+# conditioning", profiles/r05_bf16_step_cond.json) are not held to a one-step gradient
+# bound: a 2^-9 input perturbation already moves the FP32 step's own gradient by that much.
+# They are checked over a 50-step trajectory instead
+# (test_config3_bf16_trajectory_matches_fp32).
 
 
 def _param_groups(model):
@@ -440,10 +436,11 @@ def test_config3_bf16_step_matches_fp32_step(gpu_device, monkeypatch):
         bound = r["bound"]
         assert r["grad"] <= bound, (gname, bound, report)
         # the loose branch only for a group whose own fp32 sensitivity is small: a kappa
-        # above 0.01 means the fp32 step itself is ill-conditioned there and the bound
-        # would say little
-        assert (r["bound_branch"] == "tol" or r["kappa"] <= BF16_KAPPA_MAX
-                or gname in BF16_KAPPA_JUSTIFIED), (gname, report)
+        # above 0.01 means the fp32 step itself is ill-conditioned there and the one-step
+        # bound would say little; those groups are held to the fp32
+        # trajectory by test_config3_bf16_trajectory_matches_fp32
+        if r["bound_branch"] != "tol" and r["kappa"] > BF16_KAPPA_MAX:
+            r["checked_by"] = "trajectory"
         # the Adam update points the same way wherever the gradient is well conditioned
         if bound == BF16_STEP_TOL:
             assert r["update_cos"] >= 0.98, (gname, report)
@@ -468,6 +465,81 @@ def test_config3_bf16_step_matches_fp32_step(gpu_device, monkeypatch):
     for name, got, ref in (("gF", cap["gF"], gF64), ("gv", cap["gv"], gv64), ("gmu", cap["gmu"], gmu64)):
         assert_normwise(host(got).reshape(1, -1), ref.numpy().reshape(1, -1), 1e-4,
                         what=f"bf16 step: fused SO(3) {name}")
+
+
+TRAJ_STEPS = 50
+TRAJ_COS_MIN = 0.9       # groups on which the fp32 step is stable under a 2^-9 perturbation
+TRAJ_REL_SLACK = 1.25    # the others: bf16's distance <= 1.25x the perturbed fp32's
+
+
+def test_config3_bf16_trajectory_matches_fp32(gpu_device, monkeypatch):
+    """The bf16 training step against the reference-precision step over a trajectory
+    (VERDICT r5 item 6): TRAJ_STEPS DPTrainer steps (unsupervised.py:108-117: loss mean,
+    backward, global clip 1e-5, Adam lr 1e-3) from one init on the same seeded batches and
+    eps, at config 3 (B = 512, s2s2, l = 10, deconv_hidden 200), in fp32, in fp32 with the
+    input perturbed by 2^-9 each step (the fp32 trajectory's own noise floor), and in bf16
+    autocast (channels-last, every fused kernel; latent heads in fp32, vae.AMP_FP32_HEADS).
+
+    No parameter group is exempt.  Per group, the accumulated parameter change D_bf16 is
+    compared with D_f32:
+      * where the fp32 trajectory is stable (cos(D_pert, D_f32) >= TRAJ_COS_MIN: the deconv
+        stack and item_rep), cos(D_bf16, D_f32) >= TRAJ_COS_MIN;
+      * where it is not (the encoder and the mean / sigma heads: the reference's clip 1e-5 +
+        Adam turns 2^-9 input noise into cos 0.07 / 0.30 after 50 fp32 steps,
+        profiles/r06_bf16_trajectory_s2s2.json), ||D_bf16 - D_f32|| <= TRAJ_REL_SLACK x
+        ||D_pert - D_f32||: bf16 moves the trajectory no further than the fp32 step's own
+        rounding-sized perturbation does.
+    Losses: the mean over the trajectory within max(1e-2, 2x the perturbed run's
+    difference); every step within 0.1 relative."""
+    from lie_vae.experiments import vae as vae_mod
+    from lie_vae.experiments.train_dp import DPTrainer
+    from lie_vae.experiments.vae import VAE
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
+    L, B, K = 10, 512, TRAJ_STEPS
+    torch.manual_seed(0)
+    base = VAE(latent_mode="so3", decoder_mode="action", degrees=L, rep_copies=10, rgb=True,
+               batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(gpu_device)
+    base = base.to(memory_format=torch.channels_last)
+    groups = _param_groups(base)
+    p0 = {k: p.detach().clone() for k, p in base.named_parameters()}
+    gen = torch.Generator(device=gpu_device).manual_seed(1)
+    xs = [torch.rand(B, 3, 64, 64, device=gpu_device, generator=gen) for _ in range(K)]
+    es = [torch.randn(1, B, 3, device=gpu_device, generator=gen) for _ in range(K)]
+    noise = [1 + 2.0 ** -9 * torch.randn(B, 3, 64, 64, device=gpu_device, generator=gen)
+             for _ in range(K)]
+    runs = {}
+    for tag, amp, pert in (("f32", None, False), ("f32_pert", None, True), ("bf16", torch.bfloat16, False)):
+        m = copy.deepcopy(base)
+        tr = DPTrainer(m, lr=1e-3, clip_grads=1e-5, amp_dtype=amp)
+        losses = [tr.step(xs[k] * noise[k] if pert else xs[k], es[k])[0] for k in range(K)]
+        named = dict(m.named_parameters())
+        runs[tag] = {"loss": [float(x) for x in losses],
+                     "delta": {g: torch.cat([(named[n].detach() - p0[n]).flatten() for n in names]).double()
+                               for g, names in groups.items()}}
+        del m, tr
+    f, fp, b = runs["f32"], runs["f32_pert"], runs["bf16"]
+    rep = {"steps": K, "amp_fp32_heads": vae_mod.AMP_FP32_HEADS}
+    for tag, o in (("f32_pert", fp), ("bf16", b)):
+        rel = [abs(x - y) / abs(y) for x, y in zip(o["loss"], f["loss"])]
+        rep[tag] = {"loss_rel_max": max(rel), "loss_mean_rel": abs(sum(o["loss"]) - sum(f["loss"])) / sum(f["loss"])}
+        for g in groups:
+            u, w = o["delta"][g], f["delta"][g]
+            rep[tag][g] = {"cos": float(u @ w / (u.norm() * w.norm())), "rel": float((u - w).norm() / w.norm())}
+    print("config3 bf16 vs f32 trajectory:", json.dumps(rep))
+    out_dir = os.path.join(REPO, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, "bf16_trajectory_report.json"), "w") as fh:
+        json.dump(dict(rep, loss_f32=f["loss"], loss_bf16=b["loss"]), fh, indent=1)
+    assert rep["bf16"]["loss_mean_rel"] <= max(1e-2, 2 * rep["f32_pert"]["loss_mean_rel"]), rep
+    assert rep["bf16"]["loss_rel_max"] <= 0.1, rep
+    for g in groups:
+        if rep["f32_pert"][g]["cos"] >= TRAJ_COS_MIN:
+            assert rep["bf16"][g]["cos"] >= TRAJ_COS_MIN, (g, rep)
+        else:
+            assert rep["bf16"][g]["rel"] <= TRAJ_REL_SLACK * rep["f32_pert"][g]["rel"], (g, rep)
+    # the stable groups must include the decoder (the bulk of the parameters)
+    assert rep["f32_pert"]["deconv"]["cos"] >= TRAJ_COS_MIN, rep
 
 
 def test_config3_iwae_n500_vs_oracle(gpu_device):

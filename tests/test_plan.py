@@ -10,7 +10,9 @@ LDS_PER_CU = 160 * 1024
 TILE_MAX_LDS = 80 * 1024       # action.hip kTileMaxLds
 BWD_MAX_LDS = 96 * 1024        # action.hip kBwdMaxLds
 BWD_MAX_BLOCKS = 4096          # action.hip kBwdMaxBlocks
-PERSIST_MIN_GROUPS = 769       # action.hip kBwdPersistMinGroups
+CUS = _lib.load().lv_compute_units()  # the planner's CU count (256 on MI355X / no device)
+PERSIST_BLOCKS = 3 * CUS                # action_bwd_persist.h kBwdPersistBlocksPerCU
+PERSIST_MIN_GROUPS = PERSIST_BLOCKS + 1  # persistent kernel beyond one round of blocks
 F32, BF16 = _lib.LV_DTYPE_F32, _lib.LV_DTYPE_BF16
 NS = (1, 5, 6, 7, 683, 4096, 8192, 65536, 1 << 20)
 
@@ -77,7 +79,7 @@ def test_backward_plans_fit_the_kernels(L):
                     # groups; one gradient-tile buffer, 3 blocks per CU, 4 waves; workspace =
                     # one slab per block + the angle-gradient region of the fused path
                     assert C == 10 and 3 <= L <= 10 and groups >= PERSIST_MIN_GROUPS, (L, C, n)
-                    assert p["blocks"] == min(groups, 768) and p["segments"] == 4
+                    assert p["blocks"] == min(groups, PERSIST_BLOCKS) and p["segments"] == 4
                     assert 3 * p["lds_bytes"] <= LDS_PER_CU
                     assert p["aux"] == 4 * p["blocks"] * slab + 4 * 3 * n
                     assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
@@ -91,6 +93,16 @@ def test_backward_plans_fit_the_kernels(L):
                 # angle-gradient region (3 floats per sample)
                 assert p["aux"] == (4 * p["blocks"] * slab + 4 * 3 * n if shared else 0)
                 assert p["aux"] == _lib.load().lv_group_action_bwd_workspace(n, L, C, shared)
+
+
+def test_compute_units():
+    """The planner sizes the persistent grid by the device's CU count (hipDeviceAttribute-
+    MultiprocessorCount); without a device, the MI355X's 256."""
+    import torch
+    if torch.cuda.is_available():
+        assert CUS == torch.cuda.get_device_properties(0).multi_processor_count
+    else:
+        assert CUS == 256
 
 
 def test_pinned_plans_of_the_benchmark_configs():
