@@ -638,8 +638,11 @@ constexpr int kBwdReduceDefault = 6;
 // LV_BWD_VARIANT default (kBwdVar* bits): JIT chain (profiles/r04_bwd_reduce_ab.txt); the
 // persistent kernel with one tile buffer at 3 blocks per CU (65,536: 131 -> 114 us against
 // the double-buffered 2 blocks per CU, profiles/r05_ab4.txt), its next multiples filled by
-// one wave (profiles/r05_ab8.txt)
-constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1;
+// one wave (profiles/r05_ab8.txt), its angle partials summed by one wave from LDS instead of
+// a cross-lane tree on every wave (round 6, same box: 65,536 104.0 -> 96.8 us, 262,144 378
+// -> 358, 16,384 31.9 -> 30.6; the padded tile, kBwdVarPersistPad, was slower alone and
+// with it: 104.5 / 100.2-100.9 us, profiles/r06_ab_persist.txt)
+constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1 | kBwdVarPersistAng;
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
@@ -687,7 +690,8 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, int cus, BwdPlan& b) {
       b.gx = (int)std::min<int64_t>(groups, persist_blocks);
       plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
       balance_masks(L, b.nseg, true, b.seg_mask);
-      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, b.nseg, single ? 1 : 2);
+      const bool pad = single && (kEnvVariantP & kBwdVarPersistPad) != 0;
+      b.lds = sizeof(float) * (size_t)persist_lds_floats(L, b.nseg, single ? 1 : 2, pad);
       const size_t slabs = sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk);
       b.ws_gang_off = slabs;
       b.ws = slabs + sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);

@@ -635,7 +635,14 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
   if (p.persist) {
     if constexpr (LT <= kBwdPersistMaxL) {
       const bool single = (p.a.variant & kBwdVarPersistSingle) != 0;
-      if (single)
+      const int pv = ((p.a.variant & kBwdVarPersistPad) ? 1 : 0) | ((p.a.variant & kBwdVarPersistAng) ? 2 : 0);
+      if (single && pv == 3)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 3>), grid, block, p.lds, p.stream, p.a);
+      else if (single && pv == 2)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 2>), grid, block, p.lds, p.stream, p.a);
+      else if (single && pv == 1)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 1>), grid, block, p.lds, p.stream, p.a);
+      else if (single)
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true>), grid, block, p.lds, p.stream, p.a);
       else
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves>), grid, block, p.lds, p.stream, p.a);

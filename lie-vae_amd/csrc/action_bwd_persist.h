@@ -45,36 +45,58 @@ constexpr int kBwdPersistBlocksPerCUDB = 2;  // double-buffered tile (A/B)
 // CU built for 2 waves per SIMD were slower: profiles/r05_bwd_persist_ab2.txt, r05_ab4.txt,
 // r05_ab8.txt.)
 constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistTask1 = 512;
+// Round 6 (single-buffer kernel, template parameter PV): kBwdVarPersistPad = the padded
+// gradient tile (persist_pad); kBwdVarPersistAng = the angle partials leave every lane by
+// three LDS stores and one wave sums each sample's 4 x 10 (wave, column) partials after
+// the group barrier, instead of a 4-step cross-lane tree (12 ds_bpermute + ~67 VALU) on
+// every wave.
+constexpr int kBwdVarPersistPad = 1024, kBwdVarPersistAng = 2048;
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
-// Samples of the gradient tile sit M*C floats apart in LDS, exactly as in global memory, so
-// one LDS-DMA instruction moves 1 KiB of any sample(s) and the tile takes ~29 of them,
-// spread evenly over the waves.  (Padding each sample to 10 mod 64 banks removed the 2-way
-// conflicts between adjacent samples' lanes -- 0.64 conflict cycles per LDS instruction at
-// 65,536 -- but needs per-sample DMA with head / tail pieces: twice the DMA instructions,
-// ~0.05 us of issue each; 109.7 -> 109.0 us, dropped for the flat slab pass below.)
-__host__ __device__ constexpr int persist_stride(int L) { return (L + 1) * (L + 1) * 10; }
-__host__ __device__ constexpr int persist_tile_floats(int L) {
-  return (((64 / 10) * persist_stride(L) * 4 + 16 + 15) & ~15) / 4;
+// Unpadded (PAD = false), samples of the gradient tile sit M*C floats apart in LDS, exactly
+// as in global memory, so one LDS-DMA instruction moves 1 KiB of any sample(s) and the tile
+// takes ~29 of them, spread evenly over the waves.  At l = 10 that stride (1,210 floats,
+// 26 mod 32 banks) puts the 10 column lanes of adjacent samples on 4 shared banks in each
+// 32-lane half of every ds_read_b32 / ds_write_b32 of the chain (Q4 reads, dF writes): 2
+// extra LDS cycles per instruction, ~480 per group (0.64 conflict cycles per LDS
+// instruction, profiles/r05_pmc_persist_65536.txt).
+// PAD (kBwdVarPersistPad): samples persist_pad(L) floats further apart (l = 10: 1,226 =
+// 10 mod 32, so the six samples' 10-lane windows tile both halves without a shared bank).
+// The pad is a multiple of 16 bytes, so every sample's LDS image stays congruent to its
+// global image mod 16 and the tile still moves as flat 16-byte LDS-DMA pieces: a piece's
+// source is its LDS offset minus pad bytes per preceding sample (pieces in a pad read the
+// neighbouring sample's bytes into the pad, never read).
+__host__ __device__ constexpr int persist_pad(int L) {
+  return ((10 - (L + 1) * (L + 1) * 10) % 32 + 32) % 32 % 4 == 0 ? ((10 - (L + 1) * (L + 1) * 10) % 32 + 32) % 32 : 0;
 }
-__host__ __device__ constexpr int persist_lds_floats(int L, int NW, int NB = 2) {
-  return NB * persist_tile_floats(L) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
+__host__ __device__ constexpr int persist_stride(int L, bool pad = false) {
+  return (L + 1) * (L + 1) * 10 + (pad ? persist_pad(L) : 0);
+}
+__host__ __device__ constexpr int persist_tile_floats(int L, bool pad = false) {
+  return (((64 / 10) * persist_stride(L, pad) * 4 + 16 + 15) & ~15) / 4;
+}
+__host__ __device__ constexpr int persist_lds_floats(int L, int NW, int NB = 2, bool pad = false) {
+  return NB * persist_tile_floats(L, pad) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
          2 * ((((L + 1) * (L + 1) * 10) + 3) & ~3);
 }
+static_assert(persist_stride(10, true) % 32 == 10 && persist_pad(10) % 4 == 0, "l = 10 pad");
 
 // DB: double-buffered gradient tile (2 blocks per CU); else one buffer at 3 blocks per CU.
 // JIT: spectrum / gradient columns read in row pairs inside the products.
-template <int LT, int NW, bool DB = true, bool JIT = true, int WPE = (DB ? 2 : 3)>
+template <int LT, int NW, bool DB = true, bool JIT = true, int WPE = (DB ? 2 : 3), int PV = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE)))
 void action_bwd_persist_kernel(ActionBwdArgs a) {
+  constexpr bool PAD = (PV & 1) != 0 && persist_pad(LT) > 0;
+  constexpr bool ANGL = (PV & 2) != 0;
   constexpr int C = kTileFastC;
   constexpr int Sw = 64 / C;
   constexpr int MC = (LT + 1) * (LT + 1) * C;
   constexpr int MC4 = (MC + 3) & ~3;
   constexpr int kRow = TrigLds<LT>::kRow;
-  constexpr int kTile = persist_tile_floats(LT);
-  constexpr int kStride = persist_stride(LT);  // floats between samples of the tile
+  constexpr int kTile = persist_tile_floats(LT, PAD);
+  constexpr int kStride = persist_stride(LT, PAD);  // floats between samples of the tile
+  constexpr int kPadB = 4 * (kStride - MC);         // pad bytes per sample
   constexpr int kTrig = Sw * kRow;
   constexpr int kAp = NW * 64 * 3;
   constexpr int nthr = 64 * NW;
@@ -116,6 +138,30 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     const int nbytes = Sv * MC * 4;
     const char* gb = reinterpret_cast<const char*>(a.gout + s0 * MC);
     char* stage_b = reinterpret_cast<char*>(tiles + buf * kTile) + mis;
+    if constexpr (PAD) {
+      // LDS span of the padded tile: up to the last sample's data end
+      const int span = (Sv - 1) * kStride * 4 + MC * 4;
+      const int head = min((16 - mis) & 15, span);
+      const int nvec = (span - head) >> 4;
+      const int tail0 = head + nvec * 16;
+      for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
+        if (v0 + lane < nvec) {
+          // piece at LDS offset rel: the sample holding its last byte, its global bytes
+          // (a piece in a pad reads the neighbouring sample's bytes: in bounds, never used)
+          const int rel = head + 16 * (v0 + lane);
+          const int jp = (rel + 15) / (kStride * 4);
+          __builtin_amdgcn_global_load_lds(gb + rel - jp * kPadB, as_lds(stage_b + head + 16 * v0), 16, 0, 0);
+        }
+      if (wave == NW - 1) {
+        // head: the first sample's bytes (no pad before it); tail: the last sample's
+        if (4 * lane < head) __builtin_amdgcn_global_load_lds(gb + 4 * lane, as_lds(stage_b), 4, 0, 0);
+        const int tb = tail0 + 4 * lane;
+        if (tb < span)
+          __builtin_amdgcn_global_load_lds(gb + tb - (Sv - 1) * kPadB, as_lds(stage_b + tail0), 4, 0, 0);
+      }
+      (void)nbytes;
+      return;
+    }
     const int head = min((16 - mis) & 15, nbytes);
     const int nvec = (nbytes - head) >> 4;
     const int tail0 = head + nvec * 16;
@@ -311,8 +357,14 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     if (DB && task && has_next) task_fill(ang_next, nxt);
     // 5. angle partials: the C column lanes of each sample summed by a segmented
     //    cross-lane tree (((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7))) + (c8 + c9), then
-    //    one (sample, angle) value per wave into the partial buffer
-    {
+    //    one (sample, angle) value per wave into the partial buffer; (ANGL) every lane's
+    //    three partials straight to the buffer, [angle][wave][lane]
+    if constexpr (ANGL) {
+      float* ap = apart + cur * kAp + wave * 64 + lane;
+      ap[0] = ga;
+      ap[NW * 64] = gb;
+      ap[2 * NW * 64] = gc;
+    } else {
       float v0 = ga, v1 = gb, v2 = gc;
 #pragma unroll
       for (int off = 1; off < C; off <<= 1) {
@@ -339,8 +391,32 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     // 6. (one buffer) every wave is past this group's chain and slab pass: the tile takes
     //    the next group now, and the angle sums and the next multiples run under its DMA
     if (!DB && has_next) issue_tile(gn, 0);
-    // 7. the group's angle gradients (waves in order), output t on lane t / NW of wave t % NW
-    if (t_task < 3 * Sv) {
+    // 7. the group's angle gradients (waves in order), output t on lane t / NW of wave t % NW;
+    //    (ANGL) output t = (sample, angle) on lane t of wave 0: its 4 waves x 10 columns of
+    //    partials read as 8-byte pairs, summed column-pairwise then over the waves
+    if constexpr (ANGL) {
+      if (wave == 0 && lane < 3 * Sv) {
+        const int js = lane / 3, i = lane - 3 * (lane / 3);
+        // transpose: angle i is the negated sum of stored component 2 - i
+        const int ci = a.transpose ? 2 - i : i;
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const float* apc = apart + cur * kAp + ci * NW * 64 + js * C;
+        f2 pv[NW][C / 2];
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+#pragma unroll
+          for (int k = 0; k < C / 2; ++k) pv[w][k] = *reinterpret_cast<const f2*>(apc + w * 64 + 2 * k);
+        float r = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          f2 t = pv[w][0];
+#pragma unroll
+          for (int k = 1; k < C / 2; ++k) t += pv[w][k];
+          r += t[0] + t[1];
+        }
+        a.gang[(s0 + js) * 3 + i] = a.transpose ? -r : r;
+      }
+    } else if (t_task < 3 * Sv) {
       const int js = t_task / 3, i = t_task - 3 * (t_task / 3);
       const float* apc = apart + cur * kAp;
       float r = apc[js * 3 + i];
