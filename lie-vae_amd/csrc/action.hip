@@ -641,8 +641,11 @@ constexpr int kBwdReduceDefault = 6;
 // one wave (profiles/r05_ab8.txt), its angle partials summed by one wave from LDS instead of
 // a cross-lane tree on every wave (round 6, same box: 65,536 104.0 -> 96.8 us, 262,144 378
 // -> 358, 16,384 31.9 -> 30.6; the padded tile, kBwdVarPersistPad, was slower alone and
-// with it: 104.5 / 100.2-100.9 us, profiles/r06_ab_persist.txt)
-constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1 | kBwdVarPersistAng;
+// with it: 104.5 / 100.2-100.9 us, profiles/r06_ab_persist.txt), and its gradient tile
+// by buffer loads to LDS with SGPR round offsets (65,536 99.2-100.5 -> 96.8-97.5 us,
+// 4,096 13.7-13.9 -> 13.3-13.5, 262,144 359-360 -> 351-352; profiles/r06_ab_bufdma.txt)
+constexpr int kBwdVariantDefault =
+    kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1 | kBwdVarPersistAng | kBwdVarPersistBufDma;
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in
@@ -661,11 +664,14 @@ struct BwdPlan {
   size_t lds, ws;
 };
 
-// Persistent backward (action_bwd_persist.h) once the batch needs more than one round of 3
-// blocks per CU (more than 3 * CUs 6-sample groups: 769 on MI355X): 3 blocks per CU walk
-// the groups, the next group's multiples prefetched, one dF slab per block.  Below it the
-// one-group kernel (one round of blocks) is shorter (4,096: 14.26 vs 14.47 us; 9,216: 24.9
-// vs 23.1; 16,384: 38.8 vs 33.5; 65,536: 182 vs 110, profiles/r05_bwd_persist_ab2.txt).
+// Persistent backward (action_bwd_persist.h) from more than one 6-sample group per CU (257
+// groups = 1,537 samples on MI355X): up to 3 blocks per CU walk the groups, the next
+// group's multiples prefetched, one dF slab per block.  Round 5 used it only beyond one
+// round of 3 blocks per CU (769 groups; 4,096: 14.26 vs 14.47 us one-group vs persistent,
+// profiles/r05_bwd_persist_ab2.txt); with the LDS angle sums it is faster from 342 groups:
+// 2,048 samples 11.15 -> 10.5 us, 4,096 14.1 -> 13.8, while at <= one group per CU the
+// one-group kernel's 8 segments keep more waves busy (512: 8.5 vs 9.6 us, 1,024: 8.8 vs
+// 10.3; profiles/r06_ab_persist_small_batches.txt).
 
 bool plan_bwd(int64_t n, int L, int C, bool sharedF, int cus, BwdPlan& b) {
   static const int kEnvNseg = LV_KNOB("LV_BWD_NSEG", 0);      // A/B testing only
@@ -673,8 +679,10 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, int cus, BwdPlan& b) {
   static const int kEnvPersistMin = LV_KNOB("LV_BWD_PERSIST_MIN", -1);  // A/B; 0 = off, -1 = 3 * CUs + 1
   static const int kEnvVariantP = LV_KNOB("LV_BWD_VARIANT", kBwdVariantDefault);
   const bool single = (kEnvVariantP & kBwdVarPersistSingle) != 0;  // A/B: one tile buffer
-  const int64_t persist_blocks = (int64_t)cus * (single ? kBwdPersistBlocksPerCU : kBwdPersistBlocksPerCUDB);
-  const int64_t persist_min = kEnvPersistMin < 0 ? (int64_t)cus * kBwdPersistBlocksPerCU + 1 : kEnvPersistMin;
+  static const int kEnvPersistBpc = LV_KNOB("LV_BWD_PERSIST_BPC", 0);  // A/B: blocks per CU (grid)
+  const int64_t persist_blocks =
+      (int64_t)cus * (kEnvPersistBpc > 0 ? kEnvPersistBpc : single ? kBwdPersistBlocksPerCU : kBwdPersistBlocksPerCUDB);
+  const int64_t persist_min = kEnvPersistMin < 0 ? (int64_t)cus + 1 : kEnvPersistMin;
   b = BwdPlan{};
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
   if (sharedF && C == kTileFastC && L >= kBwdPersistWaves - 1 && L <= kBwdPersistMaxL && !kEnvGlobal &&

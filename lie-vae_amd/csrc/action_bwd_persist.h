@@ -51,6 +51,12 @@ constexpr int kBwdVarPersistSingle = 32, kBwdVarPersistTask1 = 512;
 // the group barrier, instead of a 4-step cross-lane tree (12 ds_bpermute + ~67 VALU) on
 // every wave.
 constexpr int kBwdVarPersistPad = 1024, kBwdVarPersistAng = 2048;
+// kBwdVarPersistBufDma: the gradient tile by buffer loads to LDS (buffer_load_dwordx4 ...
+// lds): the group's rows as a buffer resource, each lane's byte offset fixed for the whole
+// walk and the round's offset in an SGPR, so a full round of 16-byte pieces costs no VALU
+// (global_load_lds needs a 64-bit VGPR address per lane: ~5 VALU per wave instruction, ~140
+// per group); only the last, partial round keeps a per-lane bound.
+constexpr int kBwdVarPersistBufDma = 4096;
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
@@ -77,7 +83,7 @@ __host__ __device__ constexpr int persist_tile_floats(int L, bool pad = false) {
   return (((64 / 10) * persist_stride(L, pad) * 4 + 16 + 15) & ~15) / 4;
 }
 __host__ __device__ constexpr int persist_lds_floats(int L, int NW, int NB = 2, bool pad = false) {
-  return NB * persist_tile_floats(L, pad) + 2 * (64 / 10) * trig_row_floats(L) + 2 * NW * 64 * 3 +
+  return NB * persist_tile_floats(L, pad) + 2 * (64 / 10) * trig_row_floats(L) + 2 * 3 * (NW * 64 + 4) +
          2 * ((((L + 1) * (L + 1) * 10) + 3) & ~3);
 }
 static_assert(persist_stride(10, true) % 32 == 10 && persist_pad(10) % 4 == 0, "l = 10 pad");
@@ -89,6 +95,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE)))
 void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr bool PAD = (PV & 1) != 0 && persist_pad(LT) > 0;
   constexpr bool ANGL = (PV & 2) != 0;
+  constexpr bool BUFDMA = (PV & 4) != 0 && !((PV & 1) != 0 && persist_pad(LT) > 0);
   constexpr int C = kTileFastC;
   constexpr int Sw = 64 / C;
   constexpr int MC = (LT + 1) * (LT + 1) * C;
@@ -98,7 +105,11 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr int kStride = persist_stride(LT, PAD);  // floats between samples of the tile
   constexpr int kPadB = 4 * (kStride - MC);         // pad bytes per sample
   constexpr int kTrig = Sw * kRow;
-  constexpr int kAp = NW * 64 * 3;
+  // angle partials per buffer: [wave][sample][3] (tree), or (ANGL) three planes [wave][lane]
+  // kPl floats apart -- 4 floats more than a plane, so that the summing lanes' 8-byte reads
+  // of the three planes fall in distinct banks
+  constexpr int kPl = NW * 64 + 4;
+  constexpr int kAp = ANGL ? 3 * kPl : NW * 64 * 3;
   constexpr int nthr = 64 * NW;
   constexpr int NB = DB ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -165,6 +176,23 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     const int head = min((16 - mis) & 15, nbytes);
     const int nvec = (nbytes - head) >> 4;
     const int tail0 = head + nvec * 16;
+    if constexpr (BUFDMA) {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(gb), 0, nbytes, kRawBufferFlags);
+      const int vo = head + 16 * (wave * 64 + lane);  // this lane's piece in round 0
+      char* const ldsw = stage_b + head + 16 * (wave * 64);
+      const int nfull = nvec / nthr;  // rounds in which every lane of every wave has a piece
+      for (int it = 0; it < nfull; ++it)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(ldsw + it * nthr * 16), 16, vo, it * nthr * 16, 0, 0);
+      if (nfull * nthr + wave * 64 + lane < nvec)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(ldsw + nfull * nthr * 16), 16, vo, nfull * nthr * 16, 0, 0);
+      if (wave == NW - 1) {
+        if (4 * lane < head) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(stage_b), 4, 4 * lane, 0, 0, 0);
+        if (tail0 + 4 * lane < nbytes)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(stage_b + tail0), 4, 4 * lane, tail0, 0, 0);
+      }
+      return;
+    }
     for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
       if (v0 + lane < nvec)
         __builtin_amdgcn_global_load_lds(gb + head + 16 * (v0 + lane), as_lds(stage_b + head + 16 * v0), 16, 0, 0);
@@ -362,8 +390,8 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     if constexpr (ANGL) {
       float* ap = apart + cur * kAp + wave * 64 + lane;
       ap[0] = ga;
-      ap[NW * 64] = gb;
-      ap[2 * NW * 64] = gc;
+      ap[kPl] = gb;
+      ap[2 * kPl] = gc;
     } else {
       float v0 = ga, v1 = gb, v2 = gc;
 #pragma unroll
@@ -400,7 +428,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
         // transpose: angle i is the negated sum of stored component 2 - i
         const int ci = a.transpose ? 2 - i : i;
         typedef float f2 __attribute__((ext_vector_type(2)));
-        const float* apc = apart + cur * kAp + ci * NW * 64 + js * C;
+        const float* apc = apart + cur * kAp + ci * kPl + js * C;
         f2 pv[NW][C / 2];
 #pragma unroll
         for (int w = 0; w < NW; ++w)

@@ -368,7 +368,7 @@ def test_action_bwd_reproducible_and_looped(gpu_device):
         (ops.group_action(ap, fp, L) * gout[lo:lo + 4096]).sum().backward()
         ga_parts.append(ap.grad)
         gf_sum += fp.grad.double()
-    # one plan (persistent, 8,334 groups) vs 4,096-sample chunks (one-group kernel): the
+    # one plan (persistent, 8,334 groups) vs 4,096-sample chunks (683 blocks): the
     # same per-sample sums in different orders (column tree, degree split over waves)
     assert_normwise(host(a.grad), host(torch.cat(ga_parts)), 1e-4, what="looped angle grads")
     assert_normwise(host(f.grad)[None], gf_sum.cpu().numpy()[None], 1e-5, what="looped dF")
@@ -377,9 +377,9 @@ def test_action_bwd_reproducible_and_looped(gpu_device):
 def test_action_bwd_persistent_kernel(gpu_device):
     """The persistent backward (action_bwd_persist.h: 3 blocks per CU walk the 6-sample
     groups, the next group's multiples prefetched, one dF slab per block; plan mode 3 from
-    769 groups at l <= 10, C = 10, shared spectrum) at ragged large batches: bitwise
-    reproducible run to run; angle gradients and dF against 4,096-sample chunks (the
-    one-group kernel) at fp32 summation-order noise; the oracle's fp64 autograd on a
+    CUs + 1 groups at l <= 10, C = 10, shared spectrum) at ragged large batches: bitwise
+    reproducible run to run; angle gradients and dF against chunks of one group per CU
+    (the one-group kernel) at fp32 summation-order noise; the oracle's fp64 autograd on a
     sample of the batch; transposed."""
     import lie_vae._lib as lib
     import lie_vae._ops as ops
@@ -403,11 +403,12 @@ def test_action_bwd_persistent_kernel(gpu_device):
         assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1]), \
             ("persistent backward not reproducible", n)
         ga_parts, gf_sum = [], torch.zeros_like(F, dtype=torch.float64)
-        for lo in range(0, n, 4096):
-            assert lib.plan("bwd", min(4096, n - lo), L, C, 1)["tile"] == 1
-            ap = ang[lo:lo + 4096].clone().requires_grad_(True)
+        ch = 6 * lib.load().lv_compute_units()  # one group per CU: the one-group kernel
+        for lo in range(0, n, ch):
+            assert lib.plan("bwd", min(ch, n - lo), L, C, 1)["tile"] == 1
+            ap = ang[lo:lo + ch].clone().requires_grad_(True)
             fp = F.clone().requires_grad_(True)
-            (ops.group_action(ap, fp, L, transpose=transpose) * gout[lo:lo + 4096]).sum().backward()
+            (ops.group_action(ap, fp, L, transpose=transpose) * gout[lo:lo + ch]).sum().backward()
             ga_parts.append(ap.grad)
             gf_sum += fp.grad.double()
         # per-sample angle gradients are sums of ~4,000 chain terms with cancellation; the
@@ -474,12 +475,12 @@ def assert_grad_parity(y, ref32, ref64, tol=1e-4, what=""):
     assert tot(y) <= max(tol, 2 * tot(ref32)), (what, tot(y), tot(ref32))
 
 
-@pytest.mark.parametrize("n,transpose", [(4096, False), (65536, False), (30001, True)])
+@pytest.mark.parametrize("n,transpose", [(1536, False), (4096, False), (65536, False), (30001, True)])
 def test_shared_spectrum_grads_vs_oracle_fp64(gpu_device, n, transpose):
     """The shared-spectrum gradient dF and the fused path's (gmu, gv) against the oracle's
     fp64 autograd over the WHOLE batch, at the sizes where the one-group kernel + reduce5
-    (4,096: plan mode 1) and the persistent kernel (65,536 and 30,001 transposed: plan
-    mode 3) produce them.  The other backward tests compare these kernels with each other
+    (1,536 = one group per CU: plan mode 1) and the persistent kernel (4,096 with one group
+    per block, 65,536 and 30,001 transposed walking the groups: plan mode 3) produce them.  The other backward tests compare these kernels with each other
     (HIP chunks) or with the oracle on a few hundred samples; here the full reduction is
     pinned.  Tolerances: dF 1e-5 normwise over the (M, C) matrix; angle / v / mu
     gradients per sample 1e-4 normwise or the 2x rule against the reference's own fp32
@@ -489,7 +490,8 @@ def test_shared_spectrum_grads_vs_oracle_fp64(gpu_device, n, transpose):
     from oracle import lie_ref
     L, C = 10, 10
     M = (L + 1) ** 2
-    assert lib.plan("bwd", n, L, C, 1)["tile"] == (1 if n <= 4096 else 3)
+    assert lib.plan("bwd", n, L, C, 1)["tile"] == (1 if -(-n // 6) <= lib.load().lv_compute_units() else 3)
+    torch.manual_seed(4242 + n)  # haar_matrices draws from the global generator
     gen = torch.Generator().manual_seed(4242 + n)
     mu = lie_ref.haar_matrices(n)
     v = torch.randn(n, 3, generator=gen) * 0.5
@@ -567,7 +569,8 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     workspace row) keeps the LDS mode's summation order: forced on for the config-2 shape
     (LV_BWD_FGLOBAL=1, read once per process, hence a child process), the gradients are
     bitwise those of the LDS mode for the same segment plan (LV_BWD_NSEG=2 in both: the
-    LDS mode's default at this shape is the 4-segment 3-waves-per-SIMD plan).  The knobs
+    LDS mode's default at this shape is the persistent kernel, switched off here with
+    LV_BWD_PERSIST_MIN=0, and then the 4-segment 3-waves-per-SIMD plan).  The knobs
     exist only in the A/B build of the same kernels (liblievae_hip_ab.so, -DLV_AB_KNOBS);
     the product library ignores the environment (test_product_library_ignores_knobs)."""
     import subprocess
@@ -577,7 +580,7 @@ def test_action_bwd_global_spectrum_mode_bitwise(gpu_device, tmp_path):
     outs = []
     for forced in ("0", "1"):
         path = str(tmp_path / f"g{forced}.npz")
-        env = dict(os.environ, LV_BWD_FGLOBAL=forced, LV_BWD_NSEG="2",
+        env = dict(os.environ, LV_BWD_FGLOBAL=forced, LV_BWD_NSEG="2", LV_BWD_PERSIST_MIN="0",
                    LIEVAE_HIP_LIB=os.path.join(pkg, "lie_vae", "liblievae_hip_ab.so"))
         subprocess.run([sys.executable, "-c", _FGLOBAL_SCRIPT, pkg, path], env=env, check=True,
                        timeout=180)

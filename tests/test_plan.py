@@ -12,7 +12,7 @@ BWD_MAX_LDS = 96 * 1024        # action.hip kBwdMaxLds
 BWD_MAX_BLOCKS = 4096          # action.hip kBwdMaxBlocks
 CUS = _lib.load().lv_compute_units()  # the planner's CU count (256 on MI355X / no device)
 PERSIST_BLOCKS = 3 * CUS                # action_bwd_persist.h kBwdPersistBlocksPerCU
-PERSIST_MIN_GROUPS = PERSIST_BLOCKS + 1  # persistent kernel beyond one round of blocks
+PERSIST_MIN_GROUPS = CUS + 1            # persistent kernel beyond one group per CU
 F32, BF16 = _lib.LV_DTYPE_F32, _lib.LV_DTYPE_BF16
 NS = (1, 5, 6, 7, 683, 4096, 8192, 65536, 1 << 20)
 
@@ -75,7 +75,7 @@ def test_backward_plans_fit_the_kernels(L):
                 groups = -(-n // p["samples_per_group"])
                 slab = -(-MC // 16) * 16
                 if mode == 3:
-                    # persistent kernel (action_bwd_persist.h): C = 10, l <= 10, from 769
+                    # persistent kernel (action_bwd_persist.h): C = 10, l <= 10, from 257
                     # groups; one gradient-tile buffer, 3 blocks per CU, 4 waves; workspace =
                     # one slab per block + the angle-gradient region of the fused path
                     assert C == 10 and 3 <= L <= 10 and groups >= PERSIST_MIN_GROUPS, (L, C, n)
@@ -114,11 +114,14 @@ def test_pinned_plans_of_the_benchmark_configs():
     # config 5: bf16 tile (6*4410*2 + 16, rounded to 16 B) + separate fp32 spectrum copy + trig
     p = _lib.plan("fwd", 1, 0, BF16, 8192, 20, 10)
     assert (p["tile"], p["blocks"], p["lds_bytes"]) == (1, 1366, 52944 + 17640 + 3552)
-    # backward at the config-2 size: 4 segments of a 3-waves-per-SIMD build, LDS small
-    # enough for 3 blocks per CU (profiles/r02_bwd_regbudget_sweep.txt)
+    # backward at the config-2 size: the persistent kernel (one 6-sample group per block
+    # here), 4 waves, LDS small enough for 3 blocks per CU; at one group per CU or less the
+    # one-group kernel (profiles/r06_ab_persist_small_batches.txt)
     b = _lib.plan("bwd", 4096, 10, 10, 1)
-    assert (b["tile"], b["segments"], b["blocks"], b["samples_per_group"]) == (1, 4, 683, 6)
+    assert (b["tile"], b["segments"], b["blocks"], b["samples_per_group"]) == (3, 4, 683, 6)
     assert 3 * b["lds_bytes"] <= 160 * 1024
+    assert _lib.plan("bwd", 6 * CUS, 10, 10, 1)["tile"] == 1
+    assert _lib.plan("bwd", 6 * CUS + 1, 10, 10, 1)["tile"] == 3
     # config 3's batch (512, one group per CU at most): 8 segments
     assert _lib.plan("bwd", 512, 10, 10, 1)["segments"] == 8
     assert _lib.plan("bwd", 2048, 10, 10, 1)["segments"] == 4

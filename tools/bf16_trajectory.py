@@ -33,7 +33,10 @@ def run(steps=50, mean_mode="s2s2", B=512, L=10, seed=0, dev="cuda:0", heads=(2,
     from lie_vae.experiments import vae as vae_mod
     from lie_vae.experiments import nets
     nets.use_packaged_miopen_db()
-    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    torch.backends.cudnn.deterministic = os.environ.get("TRAJ_DET", "0") == "1"
+    torch.backends.cudnn.benchmark = False
+    import time
+    t0 = time.time()
     torch.manual_seed(seed)
     base = VAE(latent_mode="so3", decoder_mode="action", degrees=L, rep_copies=10, rgb=True,
                batch_norm=True, deconv_hidden=200, mean_mode=mean_mode).to(dev)
@@ -56,7 +59,7 @@ def run(steps=50, mean_mode="s2s2", B=512, L=10, seed=0, dev="cuda:0", heads=(2,
             loss, _, _ = tr.step(xs[k] * noise[k] if pert else xs[k], es[k])
             losses.append(loss.detach())
             if k % 5 == 0:
-                print(tag, "step", k, float(loss), flush=True)
+                print(tag, "step", k, float(loss), f"{time.time() - t0:.1f} s", flush=True)
         torch.cuda.synchronize()
         named = dict(m.named_parameters())
         out[tag] = {"loss": [float(x) for x in losses],

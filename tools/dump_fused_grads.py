@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import lie_vae._ops as ops  # noqa: E402
 from oracle import lie_ref  # noqa: E402  (input generation only)
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536  # noqa
 L, C, M = 10, 10, 121
 torch.manual_seed(4242 + n)
 gen = torch.Generator().manual_seed(4242 + n)
