@@ -24,7 +24,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §6):
   train_step       BASELINE config 3 (N = 1: B = 512) / config 4 (N > 1: 512 per rank,
                    RCCL bucketed all-reduce of the gradients): the full VAE training step
                    (unsupervised.py:108-117) at reference precision (fp32) and with bf16
-                   autocast, samples/s of the whole job, max over ranks
+                   autocast, samples/s of the whole job, max over ranks, the median of
+                   3 timed rounds (each round's time in the record)
+  fwd_bwd.*.roofline_valu  the group-action backward's VALU-issue roofline (it is VALU-bound
+                   at large batch): PMC VALU instructions per call at the measured FMA
+                   issue rate, as a fraction of the call time
 """
 import argparse
 import ctypes
@@ -87,7 +91,7 @@ def parse():
                     help="config-5 record: launches timed per round (0: skip the record)")
     ap.add_argument("--train-steps", type=int, default=10,
                     help="train_step record: timed steps per precision (0: skip the record)")
-    ap.add_argument("--train-warmup", type=int, default=3)
+    ap.add_argument("--train-warmup", type=int, default=5)
     ap.add_argument("--no-ang", action="store_true",
                     help="A/B only: time the instantiation without the angles output")
     ap.add_argument("--dry-run", action="store_true",
@@ -608,7 +612,7 @@ def bench_train_step(dev, env, steps, warmup):
         if cl:
             model = model.to(memory_format=torch.channels_last)
         rec = bench_train.time_train_steps(model, dev, env.world, env.rank, 512 * env.world,
-                                           steps, warmup, amp=amp)
+                                           steps, warmup, amp=amp, rounds=3)
         rec["config"]["channels_last"] = cl
         recs[tag] = rec
         del model
