@@ -55,8 +55,8 @@ F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 via v_pk_fma_f32 (= fp
 # tools/valu_rate.hip, profiles/r05_valu_rate.txt), as a fraction of the call time.
 VALU_WAVE_INSTS_PER_NS = 661.19
 BWD_VALU_PER_CALL = {  # batch -> (SQ_INSTS_VALU per call, evidence)
-    4096: (3149306 + 51604, "profiles/r06_pmc_bwd_only_4096.txt"),
-    65536: (50138643 + 84056, "profiles/r05_pmc_persist_65536.txt"),
+    4096: (3036250 + 51604, "profiles/r06_pmc_bwd_only_4096.txt"),
+    65536: (40875872 + 51604, "profiles/r06_pmc_persist_65536.txt"),
 }
 SCRUB_BYTES = 512 << 20  # > 256 MiB Infinity Cache (MI355X_MICROARCH.md:40)
 
@@ -459,10 +459,6 @@ def main():
                           f"({tj.get('measured', 'committed earlier')}), read from the file, not "
                           "measured in this run")
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(L, C, B, args.cpu_seconds)
-
     # BASELINE configs 5 and 3 / 4 as bounded sub-records of the same line (every rank
     # takes part: they are timed max over ranks like the headline)
     config5 = None
@@ -471,6 +467,13 @@ def main():
     train = None
     if args.train_steps > 0:
         train = bench_train_step(dev, env, args.train_steps, args.train_warmup)
+
+    # the CPU baseline last: ~18 s of all-thread host work right before the host-bound
+    # bf16 training step slowed that step 1.2-2.7x on the driver's box (3.9-4.3 ms per step
+    # without it in the same bench, 4.8-10.6 ms after it)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(L, C, B, args.cpu_seconds)
 
     if rank == 0:
         rec = {

@@ -57,6 +57,18 @@ constexpr int kBwdVarPersistPad = 1024, kBwdVarPersistAng = 2048;
 // (global_load_lds needs a 64-bit VGPR address per lane: ~5 VALU per wave instruction, ~140
 // per group); only the last, partial round keeps a per-lane bound.
 constexpr int kBwdVarPersistBufDma = 4096;
+// kBwdVarPersistLaneMap (with the LDS angle sums): lanes take (sample, column) pairs in the
+// order below instead of lane = 10 j + c.  With the unpadded tile at l = 10 (1,210 floats =
+// 26 mod 32 between samples) every ds_read_b32 / ds_write_b32 of the chain's tile rows had
+// 4 banks 2-way in each 32-lane half; residues 2, 3, 8, 9 hold three (j, c) pairs each, so
+// one half must keep a 2-way bank, and this assignment (found by search) leaves exactly
+// that: 1 extra LDS cycle per tile access instead of 2.  Entries are 16 j + c; lanes 60-63
+// are idle (j = 6).  Used where M*C = 26 mod 32 (l = 4, 10).
+constexpr int kBwdVarPersistLaneMap = 8192;
+static __constant__ unsigned char kPersistLaneJC[64] = {
+    0, 1, 2, 3, 5, 6, 7, 8, 9, 17, 18, 19, 21, 24, 32, 34, 37, 38, 49, 52, 53, 55,
+    57, 66, 70, 72, 73, 81, 82, 86, 87, 89, 4, 16, 20, 22, 23, 25, 33, 35, 36, 39,
+    40, 41, 48, 50, 51, 54, 56, 64, 65, 67, 68, 69, 71, 80, 83, 84, 85, 88, 96, 97, 98, 99};
 
 // LDS floats of the persistent kernel: NB gradient tiles (2: double-buffered), 2
 // multiples tables, 2 angle-partial buffers, the dF slab and the spectrum.
@@ -96,6 +108,8 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr bool PAD = (PV & 1) != 0 && persist_pad(LT) > 0;
   constexpr bool ANGL = (PV & 2) != 0;
   constexpr bool BUFDMA = (PV & 4) != 0 && !((PV & 1) != 0 && persist_pad(LT) > 0);
+  constexpr bool LMAP = (PV & 8) != 0 && ANGL && !((PV & 1) != 0 && persist_pad(LT) > 0) &&
+                        ((LT + 1) * (LT + 1) * 10) % 32 == 26;
   constexpr int C = kTileFastC;
   constexpr int Sw = 64 / C;
   constexpr int MC = (LT + 1) * (LT + 1) * C;
@@ -122,8 +136,15 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = lane / C;
-  const int c = lane - j * C;
+  int j, c;
+  if constexpr (LMAP) {
+    const int jc = kPersistLaneJC[lane];
+    j = jc >> 4;
+    c = jc & 15;
+  } else {
+    j = lane / C;
+    c = lane - j * C;
+  }
   const unsigned dmask = a.seg_mask[wave];
   const int64_t P = gridDim.x;
   const int64_t groups = a.groups;
@@ -388,7 +409,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     //    one (sample, angle) value per wave into the partial buffer; (ANGL) every lane's
     //    three partials straight to the buffer, [angle][wave][lane]
     if constexpr (ANGL) {
-      float* ap = apart + cur * kAp + wave * 64 + lane;
+      float* ap = apart + cur * kAp + wave * 64 + (j * C + c);  // [angle][wave][sample][column]
       ap[0] = ga;
       ap[kPl] = gb;
       ap[2 * kPl] = gc;
