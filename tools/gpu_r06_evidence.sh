@@ -23,6 +23,7 @@ for B in 4096 65536; do
 done
 echo "=== part 1 done"; exit 0
 fi
+step bench2 300 python bench.py --gpus 1 --steps 20 --warmup 5
 step prof_c2 600 bash tools/gpu_prof.sh c2 --batch 4096 --lmax 10 --dtype f32
 step prof_c5 600 bash tools/gpu_prof.sh c5 --batch 8192 --lmax 20 --dtype bf16
 echo "=== done"
