@@ -329,8 +329,11 @@ inline int plan_segments(int L, int nseg, double P, bool bwd, int* seg_lo) {
 // backward l = 10 segments [0,6) [6,8) [8,10) [10] ran 3.9 / 4.0 / 5.2 / 3.6 us, and every
 // wave of a block waits at the barrier for the slowest).  Each degree also carries a fixed
 // cost (multiples reads, spectrum column, LDS round trips): kDegFixed, fitted to the same
-// timings.
-constexpr double kDegFixedFwd = 40.0, kDegFixedBwd = 30.0;
+// timings; the forward's raised from 40 to 80 by the round-6 degree-set A/B
+// (profiles/r06_ab_masks_c2.txt, l = 10, 6 waves: degree 0 on the {9} wave instead of the
+// {5, 4} one, 7.09 vs 7.19 us, outputs bitwise identical).  At C = 10 (the only C with
+// degree sets) that is the one tile plan it changes.
+constexpr double kDegFixedFwd = 80.0, kDegFixedBwd = 30.0;
 inline double degree_cost_sched(int l, bool bwd) {
   return (bwd ? kDegFixedBwd : kDegFixedFwd) + degree_cost(l, bwd);
 }
@@ -408,9 +411,30 @@ unsigned long long* ab_stamps() {
   }
   return p;
 }
+// LV_TILE_MASKS (A/B): the forward tile kernel's degree sets as ':'- or ','-separated hex masks
+// (one per wave, in wave order); used only when they partition 0..L into exactly the
+// plan's wave count, so a sweep can try hand-made sets without a rebuild
+bool env_masks(int L, int nseg, unsigned* masks) {
+  const char* v = std::getenv("LV_TILE_MASKS");
+  if (!v || !*v) return false;
+  unsigned m[kMaxSeg] = {};
+  int k = 0;
+  unsigned all = 0;
+  for (const char* s = v; *s && k < kMaxSeg;) {
+    char* e = nullptr;
+    m[k] = (unsigned)std::strtoul(s, &e, 16);
+    if (e == s || (m[k] & all) || m[k] == 0) return false;
+    all |= m[k++];
+    s = (*e == ',' || *e == ':') ? e + 1 : e;
+  }
+  if (k != nseg || all != (1u << (L + 1)) - 1) return false;
+  for (int i = 0; i < kMaxSeg; ++i) masks[i] = i < nseg ? m[i] : 0u;
+  return true;
+}
 #else
 #define LV_KNOB(name, dflt) (dflt)
 inline unsigned long long* ab_stamps() { return nullptr; }
+inline bool env_masks(int, int, unsigned*) { return false; }
 #endif
 
 bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
@@ -437,7 +461,8 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   // compile-time C: cost-balanced degree sets; run-time C keeps the contiguous ranges
   // (its spectrum slices are per-wave row ranges)
   static const int kEnvContig = LV_KNOB("LV_SEG_CONTIG", 0);  // A/B: contiguous ranges everywhere
-  if (a.C == kTileFastC && !kEnvContig) balance_masks(L, nseg, false, a.seg_mask);
+  if (a.C == kTileFastC && env_masks(L, nseg, a.seg_mask)) {
+  } else if (a.C == kTileFastC && !kEnvContig) balance_masks(L, nseg, false, a.seg_mask);
   else contiguous_masks(a.seg_lo, nseg, a.seg_mask);
   // spectrum in LDS: C = kTileFastC -> the whole (M, C) once, row-major; other C ->
   // per-wave column-major slices below kTileFGlobalMinL, global memory from there
@@ -456,6 +481,8 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   a.prio = kEnvPrio;
   static const int kEnvSpread = LV_KNOB("LV_TILE_SPREAD", 0);  // A/B: prologue tasks over all waves
   a.task_spread = kEnvSpread;
+  static const int kEnvAngOrder = LV_KNOB("LV_TILE_ANG_ORDER", 0);  // A/B: 1 = angles after the spectrum loads
+  a.ang_order = kEnvAngOrder;
   p.tile = true;
   p.lds = lds;
   p.gx = (int)groups;

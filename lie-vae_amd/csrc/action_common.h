@@ -30,6 +30,8 @@ struct ActionArgs {
                         // (default); A/B: 0 off, 1 flush at 3, 3 = 2 + flush at 2
   int task_spread;      // tile kernel: prologue task t on lane t / nw of wave t % nw (1) instead
                         // of thread t (0: all tasks in wave 0)
+  int ang_order;        // tile kernel, mu-free fused: 0 = angles written before the spectrum
+                        // loads are issued (default), 1 = after them (A/B)
   unsigned long long* stamps;  // phase timestamps (A/B timeline tool; null in the product)
   int seg_lo[kMaxSeg + 1];      // non-tile kernel / run-time-C tile: contiguous degree ranges
   unsigned seg_mask[kMaxSeg];   // tile kernel: degree set of wave k (bit l = degree l)

@@ -333,7 +333,14 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     a.ang_out[(s0 + lane) * 3 + 1] = ang[1];
     a.ang_out[(s0 + lane) * 3 + 2] = ang[2];
   };
-  if (ang_lane && ang_wave == 1) write_ang();
+  // a.ang_order 0 (default): wave 1 writes the angles before it issues its spectrum loads,
+  // so its two global round trips run back to back and it reaches the prologue barrier last
+  // (timeline at 4,096: loads landed 1.08 us after wave start vs 0.52-0.68 on the other
+  // waves, barrier at 1.73 with the multiples done at 1.28); 1 (A/B): after them, so the v
+  // load and the spectrum loads are in flight together.  A/B at config 2: 7.15 / 7.16 us
+  // for 1 against 7.14 / 7.13 for 0 (profiles/r06_ab_ang_order_c2.txt) -- the other waves'
+  // chains hide the late wave, so the round-5 order stays
+  if (ang_lane && ang_wave == 1 && a.ang_order == 0) write_ang();
   // 2. spectrum staging: every load issued now (before the prologue maths), the LDS writes
   //    after it.  CT > 0: element e = tid + k * nthr of the whole (M, C) spectrum, at most
   //    kFPer per thread for the smallest block the plan makes (2 waves), a batched loop
@@ -350,6 +357,7 @@ __device__ __forceinline__ void fwd_tile_body(const ActionArgs& a, int64_t grp) 
     const int e = fbase + fstr * k;
     fv[k] = e < fcnt ? fsrc[e] : 0.f;
   }
+  if (ang_lane && ang_wave == 1 && a.ang_order != 0) write_ang();
   if (a.stamps) {  // A/B timeline: when this wave's loads (v; spectrum) have landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     phase_stamp(a.stamps, wave, 5);

@@ -518,6 +518,58 @@ def test_shared_spectrum_grads_vs_oracle_fp64(gpu_device, n, transpose):
     assert_grad_parity(host(xs[0].grad), gmu32, gmu64, what=f"fused gmu n={n}")
 
 
+_PERSIST_GRID_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import lie_vae._lib as lib
+import lie_vae._ops as ops
+d = np.load(sys.argv[2])
+dev = torch.device("cuda:0")
+ang = torch.from_numpy(d["ang"]).to(dev).requires_grad_(True)
+F = torch.from_numpy(d["F"]).to(dev).requires_grad_(True)
+gout = torch.from_numpy(d["gout"]).to(dev)
+p = lib.plan("bwd", ang.shape[0], 10, 10, 1)
+(ops.group_action(ang, F, 10) * gout).sum().backward()
+np.savez(sys.argv[3], ga=ang.grad.cpu().numpy(), gf=F.grad.cpu().numpy(), blocks=p["blocks"], tile=p["tile"])
+"""
+
+
+def test_persistent_backward_other_grid_sizes_vs_oracle(gpu_device, tmp_path):
+    """The persistent backward's grid is sized from the device's CU count (3 blocks per CU,
+    lv_compute_units), so a smaller part (a CPX partition) runs more groups per block and
+    another dF summation order.  With the A/B library's LV_BWD_PERSIST_BPC (blocks per CU)
+    the same kernel runs 1 and 2 blocks per CU on this device (256 / 512 blocks at 30,001
+    samples): dF and the angle gradients against the oracle's fp64 autograd, as the
+    product grid is (test_shared_spectrum_grads_vs_oracle_fp64)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "lie-vae_amd")
+    from oracle import lie_ref
+    n, L, C = 30001, 10, 10
+    torch.manual_seed(77)
+    gen = torch.Generator().manual_seed(77)
+    ang = lie_ref.mat_to_eazyz(lie_ref.haar_matrices(n))
+    F = torch.randn((L + 1) ** 2, C, generator=gen)
+    gout = torch.randn(n, (L + 1) ** 2, C, generator=gen)
+    inp = str(tmp_path / "in.npz")
+    np.savez(inp, ang=ang.numpy(), F=F.numpy(), gout=gout.numpy())
+    gF64, (ga64,) = _oracle_grads(None, None, ang, F, gout, L, False)
+    _, (ga32,) = _oracle_grads(None, None, ang, F, gout, L, False, torch.float32)
+    import lie_vae._lib as lib
+    cus = lib.load().lv_compute_units()
+    for bpc in (1, 2):
+        out = str(tmp_path / f"g{bpc}.npz")
+        env = dict(os.environ, LV_BWD_PERSIST_BPC=str(bpc),
+                   LIEVAE_HIP_LIB=os.path.join(pkg, "lie_vae", "liblievae_hip_ab.so"))
+        subprocess.run([sys.executable, "-c", _PERSIST_GRID_SCRIPT, pkg, inp, out], env=env, check=True,
+                       timeout=180)
+        r = np.load(out)
+        assert int(r["tile"]) == 3 and int(r["blocks"]) == bpc * cus, (bpc, int(r["blocks"]))
+        assert_normwise(r["gf"][None], gF64[None], 1e-5, what=f"dF, {bpc} blocks per CU")
+        assert_grad_parity(r["ga"], ga32, ga64, what=f"gang, {bpc} blocks per CU")
+
+
 def test_action_large_tiles_fallback_vs_oracle(gpu_device):
     """Tiles too large for the LDS plans (large C at high l; include/lievae.h plan mode 2):
     the forward's grid-stride kernel and the backward's global-spectrum fallback (dF slab
