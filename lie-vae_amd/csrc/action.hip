@@ -382,10 +382,15 @@ constexpr double kPrologueFused = 250.0;
 // bigger block); write-through (sc1) stores best while the output is small enough to be
 // written during the kernel (batch 4096, 19.8 MB), nt beyond (65536: 68 vs 81 us).
 constexpr size_t kTileMaxLds = 80 * 1024;    // >= 2 blocks per CU
-constexpr double kTileSegCostSmall = 340.0;  // per-wave chain cost target, few groups
-constexpr double kTileSegCostLarge = 560.0;  // ... many groups (>= kTileManyGroups)
+// Per-wave chain cost target by sample groups per CU (round 6, C = 10, l = 10, fp32, same
+// box: profiles/r06_ab_nseg_sweep.txt): <= 4 groups per CU 7 waves (batch 4,096: 6.92 us
+// against 7.12-7.17 at 6), <= 16 8 waves (8,192: 11.5 vs 12.0; 16,384: 17.6 vs 19.5 at 4),
+// beyond 4 waves (65,536: 60.3 vs 62.3-65.1 at 6-8; 32,768 flat from 4 to 8).
+constexpr double kTileSegCostFew = 300.0;    // -> 7 waves at l = 10
+constexpr double kTileSegCostMid = 260.0;    // -> 8
+constexpr double kTileSegCostLarge = 560.0;  // -> 4
+constexpr int64_t kTileFewGroupsPerCU = 4, kTileMidGroupsPerCU = 16;
 constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
-constexpr int64_t kTileManyGroups = 2048;
 constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
 
 // A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
@@ -437,7 +442,9 @@ inline unsigned long long* ab_stamps() { return nullptr; }
 inline bool env_masks(int, int, unsigned*) { return false; }
 #endif
 
-bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
+int device_cus();
+
+bool plan_tile(FwdLaunch& p, int L, int out_bytes, int cus) {
   static const int kEnvTile = LV_KNOB("LV_TILE", 1);
   static const int kEnvWT = LV_KNOB("LV_TILE_WT", -1);
   static const int kEnvTileNseg = LV_KNOB("LV_TILE_NSEG", 0);  // A/B testing only
@@ -451,7 +458,9 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes) {
   const int64_t groups = (a.n + Sw - 1) / Sw;
   double total = 0.0;
   for (int l = 0; l <= L; ++l) total += degree_cost(l, false);
-  const double target = groups < kTileManyGroups ? kTileSegCostSmall : kTileSegCostLarge;
+  const double target = groups <= kTileFewGroupsPerCU * cus   ? kTileSegCostFew
+                        : groups <= kTileMidGroupsPerCU * cus ? kTileSegCostMid
+                                                              : kTileSegCostLarge;
   int nseg = std::max(1, std::min(std::min(8, L + 1), (int)std::ceil(total / target)));
   if (kEnvTileNseg > 0) nseg = std::min(std::min(8, L + 1), kEnvTileNseg);
   // the prologue takes one thread per (sample, slot): 3*Sw threads of the block
@@ -521,7 +530,7 @@ int check_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int 
   return LV_OK;
 }
 
-int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C, FwdLaunch& p) {
+int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C, int cus, FwdLaunch& p) {
   if (int e = check_fwd(fused, Fstride, out_dtype, n, L, C)) return e;
   const int64_t MC = (int64_t)(L + 1) * (L + 1) * C;
   p = FwdLaunch{};
@@ -533,7 +542,7 @@ int plan_fwd(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C
   p.fused = fused;
   p.dtype = out_dtype;
   const int ob = out_dtype == LV_DTYPE_BF16 ? 2 : 4;
-  if (Fstride == 0 && plan_tile(p, L, ob)) return LV_OK;
+  if (Fstride == 0 && plan_tile(p, L, ob, cus)) return LV_OK;
   const double P = fused ? kPrologueFused : kPrologueFwd;
   static const int kEnvFwdNseg = LV_KNOB("LV_FWD_NSEG", 0);  // A/B testing only
   const int nseg = kEnvFwdNseg > 0 ? std::min(kEnvFwdNseg, std::min(L + 1, kMaxSeg))
@@ -576,16 +585,17 @@ struct PlanCache {
     used = std::min(used + 1, N);
   }
 };
-using FwdKey = std::array<int64_t, 6>;  // fused, F stride, out dtype, n, L, C
+using FwdKey = std::array<int64_t, 7>;  // fused, F stride, out dtype, n, L, C, CUs
 
 int plan_fwd_cached(bool fused, int64_t Fstride, int out_dtype, int64_t n, int L, int C, FwdLaunch& p) {
   thread_local PlanCache<FwdKey, FwdLaunch> cache;
-  const FwdKey k{fused ? 1 : 0, Fstride, out_dtype, n, L, C};
+  const int cus = device_cus();
+  const FwdKey k{fused ? 1 : 0, Fstride, out_dtype, n, L, C, cus};
   if (const FwdLaunch* hit = cache.find(k)) {
     p = *hit;
     return LV_OK;
   }
-  if (int e = plan_fwd(fused, Fstride, out_dtype, n, L, C, p)) return e;
+  if (int e = plan_fwd(fused, Fstride, out_dtype, n, L, C, cus, p)) return e;
   cache.put(k, p);
   return LV_OK;
 }
@@ -1010,7 +1020,7 @@ int lv_action_fwd_plan(int fused, int64_t F_batch_stride, int out_dtype, int64_t
   LV_CHECK_ARG(plan, "null plan");
   LV_CHECK_ARG(n > 0, "n must be > 0 (got %lld)", (long long)n);
   FwdLaunch p;
-  if (int e = plan_fwd(fused != 0, F_batch_stride, out_dtype, n, L, C, p)) return e;
+  if (int e = plan_fwd(fused != 0, F_batch_stride, out_dtype, n, L, C, device_cus(), p)) return e;
   plan[0] = p.tile ? 1 : 0;
   plan[1] = p.gx;
   plan[2] = p.gy;

@@ -469,7 +469,8 @@ def test_config3_bf16_step_matches_fp32_step(gpu_device, monkeypatch):
 
 TRAJ_STEPS = 50
 TRAJ_COS_MIN = 0.9   # groups on which the fp32 step is stable under a 2^-9 input perturbation
-TRAJ_NORM_BAND = 2.0  # the others: bf16's accumulated change within 2x of fp32's, either way
+TRAJ_NORM_BAND = 2.0  # the others: bf16's accumulated change within 2x of the scale spread
+                      # the perturbed fp32 runs themselves show, either way
 
 
 def test_config3_bf16_trajectory_matches_fp32(gpu_device, monkeypatch):
@@ -490,9 +491,11 @@ def test_config3_bf16_trajectory_matches_fp32(gpu_device, monkeypatch):
         clip 1e-5 most per-parameter gradients sit near Adam's eps = 1e-8, and a 2^-9 input
         perturbation leaves cos 0.07-0.21 / -0.12-0.66 after 50 fp32 steps,
         profiles/r06_bf16_trajectory_s2s2.json), no run can track the fp32 direction, bf16
-        or fp32; the check is that bf16 moves the group on the same scale:
-        1/TRAJ_NORM_BAND <= |D_bf16| / |D_f32| <= TRAJ_NORM_BAND (measured 1.1-1.4: bf16
-        rounding noise lifts tiny gradients out of the eps-dominated regime).
+        or fp32; the check is that bf16 moves the group on the same scale as fp32 does
+        under the perturbation: with s = the perturbed runs' largest max(r, 1/r) of
+        r = |D_pert| / |D_f32|, 1/(TRAJ_NORM_BAND s) <= |D_bf16| / |D_f32| <= TRAJ_NORM_BAND s
+        (measured: the heads' r reaches 2.9-3.5 in fp32 itself from run to run, bf16 0.6-2.7;
+        bf16 rounding noise lifts tiny gradients out of the eps-dominated regime).
     Losses: the mean over the trajectory within 2e-2 relative and within 16x the
     perturbed runs' own difference (the one-step test's 16-kappa factor: bf16 rounds ~80
     times along a gradient path, the perturbation once); every step within 0.25 (the
@@ -564,7 +567,9 @@ def test_config3_bf16_trajectory_matches_fp32(gpu_device, monkeypatch):
         if g in stable:
             assert rep["bf16"][g]["cos"] >= TRAJ_COS_MIN, (g, rep)
         else:
-            assert 1 / TRAJ_NORM_BAND <= rep["bf16"][g]["norm_ratio"] <= TRAJ_NORM_BAND, (g, rep)
+            spread = max(max(rep[t][g]["norm_ratio"], 1 / rep[t][g]["norm_ratio"]) for t in ("f32_pert", "f32_pert2"))
+            band = TRAJ_NORM_BAND * spread
+            assert 1 / band <= rep["bf16"][g]["norm_ratio"] <= band, (g, band, rep)
 
 
 def test_config3_iwae_n500_vs_oracle(gpu_device):

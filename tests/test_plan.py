@@ -111,6 +111,11 @@ def test_pinned_plans_of_the_benchmark_configs():
     p = _lib.plan("fwd", 1, 0, F32, 4096, 10, 10)
     assert (p["tile"], p["blocks"], p["lds_bytes"], p["aux"]) == (1, 683, 30880, 1)
     assert _lib.plan("fwd", 1, 0, F32, 65536, 10, 10)["aux"] == 0  # > 24 MB: nt stores
+    # waves per block by sample groups per CU (profiles/r06_ab_nseg_sweep.txt): 7 up to 4
+    # groups per CU, 8 up to 16, 4 beyond
+    for n, waves in ((4096, 7), (4 * 6 * CUS, 7), (4 * 6 * CUS + 6, 8), (16384, 8),
+                     (16 * 6 * CUS, 8), (16 * 6 * CUS + 6, 4), (65536, 4)):
+        assert _lib.plan("fwd", 1, 0, F32, n, 10, 10)["segments"] == waves, n
     # config 5: bf16 tile (6*4410*2 + 16, rounded to 16 B) + separate fp32 spectrum copy + trig
     p = _lib.plan("fwd", 1, 0, BF16, 8192, 20, 10)
     assert (p["tile"], p["blocks"], p["lds_bytes"]) == (1, 1366, 52944 + 17640 + 3552)
