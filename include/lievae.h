@@ -284,6 +284,16 @@ int lv_deconv4s2_fwd_bf16_ex(const void* x, const void* wt, const float* bias, v
 int lv_deconv4s2_small_bwd_bf16_ex(const void* x, const void* gy, const void* wd, void* gx, void* gw,
                                    float* gb, float* ws, int64_t N, int H, int W, int Cin, int Cout,
                                    int flags, void* stream);
+/* The same layer in fp32 (the reference trains in fp32: unsupervised.py:108-117), on fp32
+ * MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulate).  x channels-last
+ * (N, H, W, Cin) fp32, y NCHW (N, Cout, 2H, 2W) fp32; Cin % 4 == 0, 1 <= Cout <= 208.  The
+ * weight (Cin, Cout, 4, 4) fp32 repacked into lv_deconv4s2_packed_weight_elems_f32(Cin)
+ * floats; bias (Cout) or NULL; flags 0 or LV_DECONV_RELU_OUT.  y_cl (or NULL, Cout % 4 == 0):
+ * the same output also channels-last (N, 2H, 2W, Cout), e.g. the next such layer's x. */
+size_t lv_deconv4s2_packed_weight_elems_f32(int Cin);
+int lv_deconv4s2_pack_weight_f32(const float* w, float* wt, int Cin, int Cout, void* stream);
+int lv_deconv4s2_fwd_f32(const float* x, const float* wt, const float* bias, float* y, float* y_cl,
+                         int64_t N, int H, int W, int Cin, int Cout, int flags, void* stream);
 
 #ifdef __cplusplus
 }

@@ -416,11 +416,12 @@ unsigned long long* ab_stamps() {
   }
   return p;
 }
-// LV_TILE_MASKS (A/B): the forward tile kernel's degree sets as ':'- or ','-separated hex masks
-// (one per wave, in wave order); used only when they partition 0..L into exactly the
-// plan's wave count, so a sweep can try hand-made sets without a rebuild
-bool env_masks(int L, int nseg, unsigned* masks) {
-  const char* v = std::getenv("LV_TILE_MASKS");
+// LV_TILE_MASKS / LV_BWD_MASKS (A/B): the forward tile kernel's / the compile-time-C
+// backward's degree sets as ':'- or ','-separated hex masks (one per wave, in wave order);
+// used only when they partition 0..L into exactly the plan's wave count, so a sweep can try
+// hand-made sets without a rebuild
+bool env_masks(const char* name, int L, int nseg, unsigned* masks) {
+  const char* v = std::getenv(name);
   if (!v || !*v) return false;
   unsigned m[kMaxSeg] = {};
   int k = 0;
@@ -439,7 +440,7 @@ bool env_masks(int L, int nseg, unsigned* masks) {
 #else
 #define LV_KNOB(name, dflt) (dflt)
 inline unsigned long long* ab_stamps() { return nullptr; }
-inline bool env_masks(int, int, unsigned*) { return false; }
+inline bool env_masks(const char*, int, int, unsigned*) { return false; }
 #endif
 
 int device_cus();
@@ -470,7 +471,7 @@ bool plan_tile(FwdLaunch& p, int L, int out_bytes, int cus) {
   // compile-time C: cost-balanced degree sets; run-time C keeps the contiguous ranges
   // (its spectrum slices are per-wave row ranges)
   static const int kEnvContig = LV_KNOB("LV_SEG_CONTIG", 0);  // A/B: contiguous ranges everywhere
-  if (a.C == kTileFastC && env_masks(L, nseg, a.seg_mask)) {
+  if (a.C == kTileFastC && env_masks("LV_TILE_MASKS", L, nseg, a.seg_mask)) {
   } else if (a.C == kTileFastC && !kEnvContig) balance_masks(L, nseg, false, a.seg_mask);
   else contiguous_masks(a.seg_lo, nseg, a.seg_mask);
   // spectrum in LDS: C = kTileFastC -> the whole (M, C) once, row-major; other C ->
@@ -734,7 +735,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, int cus, BwdPlan& b) {
       b.groups = groups;
       b.gx = (int)std::min<int64_t>(groups, persist_blocks);
       plan_segments(L, b.nseg, kTilePrologue, true, b.seg_lo);
-      balance_masks(L, b.nseg, true, b.seg_mask);
+      if (!env_masks("LV_BWD_MASKS", L, b.nseg, b.seg_mask)) balance_masks(L, b.nseg, true, b.seg_mask);
       const bool pad = single && (kEnvVariantP & kBwdVarPersistPad) != 0;
       b.lds = sizeof(float) * (size_t)persist_lds_floats(L, b.nseg, single ? 1 : 2, pad);
       const size_t slabs = sizeof(float) * (size_t)b.gx * (size_t)(slab_chunks(MC) * kSlabChunk);
@@ -767,7 +768,7 @@ bool plan_bwd(int64_t n, int L, int C, bool sharedF, int cus, BwdPlan& b) {
       const bool ct = C == kTileFastC && fmode == kBwdFShared;
       static const int kEnvContig = LV_KNOB("LV_SEG_CONTIG", 0);  // A/B: contiguous ranges everywhere
       if ((fmode == kBwdFShared && !ct) || kEnvContig) contiguous_masks(b.seg_lo, nseg, b.seg_mask);
-      else balance_masks(L, nseg, true, b.seg_mask);
+      else if (!(ct && env_masks("LV_BWD_MASKS", L, nseg, b.seg_mask))) balance_masks(L, nseg, true, b.seg_mask);
       int fp = 0;
       if (fmode == kBwdFShared && !ct)
         for (int k = 0; k < nseg; ++k) fp = std::max(fp, fseg_rows(b.seg_lo[k], b.seg_lo[k + 1]) * C);

@@ -440,6 +440,215 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
   }
 }
 
+// ----------------------------------------------------- fp32 (the reference's precision)
+// The same four sub-pixel GEMMs for fp32 operands on v_mfma_f32_16x16x4_f32 (exact fp32
+// products, fp32 accumulation), for the fp32 training step (reference unsupervised.py:108-117
+// trains in fp32), where MIOpen runs these layers at 53% of the fp32 peak
+// (profiles/r06_conv_layers_f32.txt).  x is channels-last (N, H, W, Cin) fp32, y NCHW fp32
+// (the layout of the fp32 network around it).  The v2 structure with fp32 elements: K steps
+// of 16 (64-byte rows per stage, as the bf16 kernel's 32), LDS-DMA ring of 2 stages with the
+// same XOR-swizzled 16-byte chunks, 8 waves as (BM / 64) x (8 / (BM / 64)), XCD-grouped
+// phases.  A lane's 16-byte fragment (k = 4 kc .. 4 kc + 3 of its row) feeds four MFMAs:
+// MFMA `sub` takes k = 4 kc + sub from lane group kc, in A and B alike.  The epilogue stages
+// one 64-row band per pass in LDS (pitch kBN + 1: conflict-free reads) and writes NCHW
+// with one 4-byte store per element, consecutive lanes on consecutive pixels.
+constexpr int kBKf = 16;
+template <int BM, int S = 2>
+struct DeconvF32 {
+  static constexpr int kWM = BM / 64, kWN = 8 / kWM;
+  static constexpr int kNW = (kNT + kWN - 1) / kWN;
+  static constexpr int kAI = BM / 128;                     // A DMA instructions per wave
+  static constexpr int kA = BM * kBKf, kB = kBN * kBKf;    // floats per stage
+  static constexpr int kSP = kBN + 1;                      // epilogue stage pitch (floats)
+  static constexpr size_t kRing = S * (size_t)(kA + kB) * 4;
+  static constexpr size_t kStage = 64 * (size_t)kSP * 4;
+  static constexpr size_t kLds = kRing > kStage ? kRing : kStage;  // BM 128: 53,504 B
+};
+
+// Wt[p][o][t*Cin + c] = w[c][o][ku][kv] in fp32 (deconv_pack_kernel's layout), 4 k per thread
+// (one 16-byte store), + 16 zero floats after it (the source of taps outside the image).
+__global__ void deconv_pack_f32_kernel(const float* w, float* wt, int Cin, int Cout) {
+  const int K = 4 * Cin, kg = K / 4;
+  const int total = 4 * kBN * kg;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i % kg, o = (i / kg) % kBN, p = i / (kg * kBN);
+    const int k0 = 4 * g, t = k0 / Cin, c0 = k0 - t * Cin;
+    const int r = p >> 1, s = p & 1;
+    const int di = r - 1 + (t >> 1), dj = s - 1 + (t & 1);
+    const int tap = (1 - 2 * di + r) * 4 + (1 - 2 * dj + s);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = o < Cout ? w[((c0 + e) * Cout + o) * 16 + tap] : 0.f;
+    *reinterpret_cast<f32x4*>(wt + ((int64_t)(p * kBN + o) * K + k0)) = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 4)
+    *reinterpret_cast<f32x4*>(wt + (int64_t)4 * kBN * K + 4 * threadIdx.x) = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+struct DeconvF32Args {
+  const float* x;     // (N, H, W, Cin) fp32, channels-last
+  const float* wt;    // (4, kBN, 4*Cin) fp32, deconv_pack_f32_kernel
+  const float* bias;  // (Cout) or null
+  float* y;           // (N, Cout, 2H, 2W) fp32, NCHW
+  float* y_cl;        // the same values channels-last (N, 2H, 2W, Cout), or null
+  int64_t M;          // N*H*W pixels per phase
+  int H, W, Cin, Cout;
+  int relu;
+};
+
+template <int BM, int S>
+__global__ __launch_bounds__(512) void deconv_mfma_f32_kernel(DeconvF32Args a) {
+  using T = DeconvF32<BM, S>;
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / T::kWN, wn = wave % T::kWN;
+  const int t0 = wn * kNT / T::kWN, ntw = (wn + 1) * kNT / T::kWN - t0;
+  // XCD-grouped 1-D grid (deconv_mfma2_kernel): phases of a tile on one XCD
+  const int bid = (int)blockIdx.x, slot = bid >> 3;
+  const int p = slot & 3;
+  const int tile = (bid & 7) + 8 * (slot >> 2);
+  if ((int64_t)tile * BM >= a.M) return;
+  const int r = p >> 1, s = p & 1;
+  const int64_t m0 = (int64_t)tile * BM;
+  const int K = 4 * a.Cin;
+  const int nk = K / kBKf;
+  const float* wtp = a.wt + (int64_t)p * kBN * K;
+  const float* zero16 = a.wt + (int64_t)4 * kBN * K;
+  const int lrow = lane >> 2, lslot = lane & 3;
+  int64_t abase[T::kAI];
+  int aa[T::kAI], ab[T::kAI], achunk[T::kAI];
+#pragma unroll
+  for (int i = 0; i < T::kAI; ++i) {
+    const int row = (BM / 8) * wave + 16 * i + lrow;
+    achunk[i] = v2_swz(row, lslot);
+    const int64_t m = m0 + row;
+    if (m < a.M) {
+      const int64_t na = m / a.W;
+      ab[i] = (int)(m - na * a.W);
+      aa[i] = (int)(na % a.H);
+      abase[i] = (na / a.H) * a.H;
+    } else {
+      abase[i] = -1;
+      aa[i] = ab[i] = 0;
+    }
+  }
+  const int nbg = wave + 8 < kNT ? 2 : 1;
+  const int bchunk = v2_swz(lrow, lslot);
+  auto issue = [&](int ks, int stage) {
+    float* As = smf + stage * (T::kA + T::kB);
+    float* Bs = As + T::kA;
+#pragma unroll
+    for (int i = 0; i < T::kAI; ++i) {
+      const int k0 = ks * kBKf + achunk[i] * 4;
+      const int t = k0 / a.Cin, c = k0 - t * a.Cin;
+      const int ia = aa[i] + r - 1 + (t >> 1), ib = ab[i] + s - 1 + (t & 1);
+      const float* src = (abase[i] >= 0 && ia >= 0 && ia < a.H && ib >= 0 && ib < a.W)
+                             ? a.x + ((abase[i] + ia) * a.W + ib) * a.Cin + c
+                             : zero16;
+      __builtin_amdgcn_global_load_lds(src, as_lds(As + ((BM / 8) * wave + 16 * i) * kBKf), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j < nbg) {
+        const int g = wave + 8 * j;
+        const float* src = wtp + (int64_t)(16 * g + lrow) * K + ks * kBKf + bchunk * 4;
+        __builtin_amdgcn_global_load_lds(src, as_lds(Bs + 16 * g * kBKf), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[4][T::kNW];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < T::kNW; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) issue(st, st);
+  const int per = T::kAI + nbg;  // DMA instructions per stage of this wave
+  const int fr = lane & 15, kc = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int stage = ks % S;
+    vm_wait(per * min(S - 2, nk - 1 - ks));  // this wave's pieces of step ks have landed
+    // everyone's have; stage (ks - 1) % S is free
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (ks + S - 1 < nk) issue(ks + S - 1, (ks + S - 1) % S);
+    const float* As = smf + stage * (T::kA + T::kB);
+    const float* Bs = As + T::kA;
+    f32x4 af[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int row = wm * 64 + mt * 16 + fr;
+      af[mt] = *reinterpret_cast<const f32x4*>(As + row * kBKf + v2_swz(row, kc) * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < T::kNW; ++j) {
+      if (j < ntw) {
+        const int row = (t0 + j) * 16 + fr;
+        const f32x4 bf = *reinterpret_cast<const f32x4*>(Bs + row * kBKf + v2_swz(row, kc) * 4);
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mt][sub], bf[sub], acc[mt][j], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: + bias (+ ReLU), one 64-row band (wave row wm) per pass staged [row][o], then
+  // NCHW stores: element e of the band -> (o = e / 64, row = e % 64)
+  float* Cs = smf;
+  const int cq = (lane >> 4) * 4;
+  const int H2 = 2 * a.H, W2 = 2 * a.W;
+  for (int pass = 0; pass < T::kWM; ++pass) {
+    __syncthreads();
+    if (wm == pass) {
+#pragma unroll
+      for (int j = 0; j < T::kNW; ++j) {
+        if (j < ntw) {
+          const int o = (t0 + j) * 16 + fr;
+          const float bo = (a.bias && o < a.Cout) ? a.bias[o] : 0.f;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float v = acc[mt][j][q] + bo;
+              if (a.relu) v = fmaxf(v, 0.f);
+              Cs[(mt * 16 + cq + q) * T::kSP + o] = v;
+            }
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * a.Cout; e += 512) {
+      const int row = e & 63, o = e >> 6;
+      const int64_t m = m0 + pass * 64 + row;
+      if (m >= a.M) continue;
+      const int64_t na = m / a.W;
+      const int b = (int)(m - na * a.W);
+      const int aa_ = (int)(na % a.H);
+      const int64_t n = na / a.H;
+      a.y[((n * a.Cout + o) * H2 + 2 * aa_ + r) * W2 + 2 * b + s] = Cs[row * T::kSP + o];
+    }
+    if (a.y_cl) {  // channels-last twin (the next layer's input): 16-byte pieces of 4 channels
+      const int q4 = a.Cout >> 2;
+      for (int e = tid; e < 64 * q4; e += 512) {
+        const int row = e / q4, q = e - row * q4;
+        const int64_t m = m0 + pass * 64 + row;
+        if (m >= a.M) continue;
+        const int64_t na = m / a.W;
+        const int b = (int)(m - na * a.W);
+        const int aa_ = (int)(na % a.H);
+        const int64_t n = na / a.H;
+        const float* src = Cs + row * T::kSP + 4 * q;
+        *reinterpret_cast<f32x4*>(a.y_cl + ((n * H2 + 2 * aa_ + r) * W2 + 2 * b + s) * a.Cout + 4 * q) =
+            f32x4{src[0], src[1], src[2], src[3]};
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------- small-Cout decoder layer
 // The decoder's last layer ConvTranspose2d(200, 3, 4, 2, 1) (nets.py:74): an N = 3
 // GEMM per phase wastes an MFMA tile and MIOpen runs it at ~10 TFLOP/s (1 ms per forward
@@ -1010,6 +1219,16 @@ using namespace lv;
 // 256-row tiles' 38 / 74 / 284 and v1's 43 / 88 / 344, all bitwise equal
 // (profiles/r03_deconv_v2.txt).
 constexpr int kDeconvAutoBM = 6;
+constexpr int kDeconvF32Default = 1;
+#ifdef LV_AB_KNOBS
+int deconv_env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+#define LV_DECONV_KNOB(name, dflt) deconv_env_int(name, dflt)
+#else
+#define LV_DECONV_KNOB(name, dflt) (dflt)
+#endif
 
 namespace {
 template <int S, bool XCD, int BM = 256>
@@ -1022,6 +1241,13 @@ int launch_deconv_v2(const DeconvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((deconv_mfma2_kernel<S, false, BM>), dim3((unsigned)tiles, 4), dim3(512),
                        (DeconvV2<S, BM>::kLds), st, a);
   LV_RETURN_LAUNCH("deconv_mfma2_kernel");
+}
+template <int BM, int S>
+int launch_deconv_f32(const DeconvF32Args& a, hipStream_t st) {
+  const int64_t tiles = (a.M + BM - 1) / BM;
+  hipLaunchKernelGGL((deconv_mfma_f32_kernel<BM, S>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
+                     (DeconvF32<BM, S>::kLds), st, a);
+  LV_RETURN_LAUNCH("deconv_mfma_f32_kernel");
 }
 template <int BM>
 int launch_deconv(const DeconvArgs& a, hipStream_t st) {
@@ -1093,6 +1319,43 @@ int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias,
 int lv_deconv4s2_fwd_bf16_ex(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                              int H, int W, int Cin, int Cout, int flags, void* stream) {
   return deconv_fwd(x, wt, bias, y, N, H, W, Cin, Cout, 0, flags, stream);
+}
+
+size_t lv_deconv4s2_packed_weight_elems_f32(int Cin) { return 4 * (size_t)kBN * 4 * (size_t)Cin + 16; }
+
+int lv_deconv4s2_pack_weight_f32(const float* w, float* wt, int Cin, int Cout, void* stream) {
+  clear_error();
+  LV_CHECK_ARG(w && wt, "null pointer");
+  LV_CHECK_ARG(Cin > 0 && Cin % 4 == 0, "Cin must be a positive multiple of 4 (got %d)", Cin);
+  LV_CHECK_ARG(Cout > 0 && Cout <= kBN, "Cout must be in [1, %d] (got %d)", kBN, Cout);
+  LV_CHECK_ARG((int64_t)Cin * Cout * 16 < (1ll << 31), "weight too large");
+  hipLaunchKernelGGL(deconv_pack_f32_kernel, dim3(ceil_div(4 * kBN * Cin, 256)), dim3(256), 0, (hipStream_t)stream,
+                     w, wt, Cin, Cout);
+  LV_RETURN_LAUNCH("deconv_pack_f32_kernel");
+}
+
+int lv_deconv4s2_fwd_f32(const float* x, const float* wt, const float* bias, float* y, float* y_cl, int64_t N,
+                         int H, int W, int Cin, int Cout, int flags, void* stream) {
+  clear_error();
+  LV_CHECK_ARG((flags & ~LV_DECONV_RELU_OUT) == 0, "flags: only LV_DECONV_RELU_OUT for this layer");
+  LV_CHECK_ARG(N >= 0 && H > 0 && W > 0, "bad shape");
+  LV_CHECK_ARG(Cin > 0 && Cin % 4 == 0, "Cin must be a positive multiple of 4 (got %d)", Cin);
+  LV_CHECK_ARG(Cout > 0 && Cout <= kBN, "Cout must be in [1, %d] (got %d)", kBN, Cout);
+  if (N == 0) return LV_OK;
+  LV_CHECK_ARG(x && wt && y, "null pointer");
+  LV_CHECK_ARG(!y_cl || Cout % 4 == 0, "the channels-last twin needs Cout %% 4 == 0 (got %d)", Cout);
+  const int64_t M = N * H * W;
+  LV_CHECK_ARG(N * Cout * 4 * H * W < (1ll << 40) && (M + 127) / 128 * 4 + 32 <= 0x7fffffff, "batch too large");
+  DeconvF32Args a{x, wt, bias, y, y_cl, M, H, W, Cin, Cout, (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
+  // A/B build: LV_DECONV_F32_VARIANT 1 = 128-row tiles, 2-stage ring (the default); 2 = 3
+  // stages; 3 = 256-row tiles, 2 stages; 4 = 256 rows, 3 stages
+  static const int kVar = LV_DECONV_KNOB("LV_DECONV_F32_VARIANT", kDeconvF32Default);
+  switch (kVar) {
+    case 2: return launch_deconv_f32<128, 3>(a, (hipStream_t)stream);
+    case 3: return launch_deconv_f32<256, 2>(a, (hipStream_t)stream);
+    case 4: return launch_deconv_f32<256, 3>(a, (hipStream_t)stream);
+    default: return launch_deconv_f32<128, 2>(a, (hipStream_t)stream);
+  }
 }
 
 size_t lv_deconv4s2_small_packed_weight_elems(int Cin) { return (size_t)((Cin + 31) / 32) * 9 * 16 * 32; }

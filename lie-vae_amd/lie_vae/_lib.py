@@ -75,16 +75,20 @@ _SIGS["lv_deconv4s2_small_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I
 _SIGS["lv_deconv4s2_fwd_bf16_ex"] = [_P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 _SIGS["lv_deconv4s2_small_bwd_bf16_ex"] = [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 LV_DECONV_RELU_OUT, LV_DECONV_MASK_GX = 1, 4  # include/lievae.h
+_SIGS["lv_deconv4s2_pack_weight_f32"] = [_P, _P, _I, _I, _P]
+_SIGS["lv_deconv4s2_fwd_f32"] = [_P, _P, _P, _P, _P, _I64, _I, _I, _I, _I, _I, _P]
 _SIGS["lv_channel_sum_bf16"] = [_P, _P, _P, _I64, _I, _P]
 _SIGS["lv_accumulate_bf16_f32"] = [_P, _P, _I64, _P]
 _SIGS["lv_bn_lrelu_fwd_bf16"] = [_P, _P, _P, _P, _P, _I, _F, _F, _F, _P, _P, _P, _P, _I64, _I, _P]
 _SIGS["lv_bn_lrelu_bwd_bf16"] = [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I64, _I, _P]
 _RESTYPES = {"lv_group_action_bwd_workspace": _SZ, "lv_last_error": ctypes.c_char_p,
              "lv_deconv4s2_packed_weight_elems": _SZ, "lv_deconv4s2_small_packed_weight_elems": _SZ,
+             "lv_deconv4s2_packed_weight_elems_f32": _SZ,
              "lv_deconv4s2_small_dgrad_weight_elems": _SZ, "lv_deconv4s2_small_bwd_workspace_elems": _SZ,
              "lv_channel_sum_workspace_elems": _SZ, "lv_bn_workspace_elems": _SZ}
 _SIGS_EXTRA = {"lv_group_action_bwd_workspace": [_I64, _I, _I, _I], "lv_last_error": [],
                "lv_deconv4s2_packed_weight_elems": [_I], "lv_deconv4s2_small_packed_weight_elems": [_I],
+               "lv_deconv4s2_packed_weight_elems_f32": [_I],
                "lv_deconv4s2_small_dgrad_weight_elems": [_I],
                "lv_deconv4s2_small_bwd_workspace_elems": [_I64, _I, _I, _I, _I],
                "lv_channel_sum_workspace_elems": [_I64, _I],

@@ -410,6 +410,60 @@ class _Deconv4s2(torch.autograd.Function):
         return gx, _like(gw, ctx.w_cl), (_channel_sum(gy) if need_b else None), None
 
 
+# fp32 (the reference's precision, no autocast): the k4 s2 p1 layers with 4 < Cout <= 208
+# run their forward on lv_deconv4s2_fwd_f32 (fp32 MFMA) instead of MIOpen; their backward
+# stays aten.convolution_backward (MIOpen), as for nn.ConvTranspose2d.
+MFMA_DECONV_F32 = True
+
+
+class _Deconv4s2F32(torch.autograd.Function):
+    """y = conv_transpose2d(x, w, b, stride 2, padding 1), k = 4, fp32 NCHW in and out: the
+    forward on lv_deconv4s2_fwd_f32 (x read channels-last: one transposing copy), with
+    LV_DECONV_RELU_OUT returning relu(y) (the backward then masks gy by y > 0, unless
+    SKIP_MASK: the consumer of y returns a masked gradient).  Backward: gx, gw, gb by
+    aten.convolution_backward on the saved fp32 operands, what nn.ConvTranspose2d runs."""
+
+    last_twin = None  # the channels-last twin of the latest forward's y (see MfmaConvTranspose2d)
+
+    @staticmethod
+    def forward(ctx, x, w, b, flags=0, x_cl=None, twin=False):
+        from .. import _lib
+        N, Cin, H, W = x.shape
+        Cout = w.shape[1]
+        wc = w.contiguous()
+        st = _lib.stream()
+        wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems_f32(Cin), device=x.device,
+                         dtype=torch.float32)
+        _lib.call("lv_deconv4s2_pack_weight_f32", wc.data_ptr(), wt.data_ptr(), Cin, Cout, st)
+        xc = x_cl if x_cl is not None else x.contiguous(memory_format=torch.channels_last)
+        y = torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=torch.float32)
+        ycl = (torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=torch.float32,
+                           memory_format=torch.channels_last) if twin else None)
+        _Deconv4s2F32.last_twin = ycl
+        _lib.call("lv_deconv4s2_fwd_f32", xc.data_ptr(), wt.data_ptr(), None if b is None else b.data_ptr(),
+                  y.data_ptr(), None if ycl is None else ycl.data_ptr(), N, H, W, Cin, Cout,
+                  flags & _lib.LV_DECONV_RELU_OUT, st)
+        relu_out = bool(flags & _lib.LV_DECONV_RELU_OUT) and not flags & _Deconv4s2.SKIP_MASK
+        ctx.save_for_backward(x, wc, *((y,) if relu_out else ()))
+        ctx.has_bias = b is not None
+        ctx.relu_out = relu_out
+        ctx.w_cl = _cl(w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors[:2]
+        Cout = w.shape[1]
+        if ctx.relu_out:
+            gy = torch.ops.aten.threshold_backward(gy, ctx.saved_tensors[2], 0)
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        need_b = need_b and ctx.has_bias
+        gx, gw, gb = torch.ops.aten.convolution_backward(
+            gy, x, w, [Cout] if need_b else None, [2, 2], [1, 1], [1, 1], True, [0, 0], 1,
+            [need_x, need_w, need_b])
+        return gx, _like(gw, ctx.w_cl), gb, None, None, None
+
+
 def _like(g, channels_last):
     """A weight gradient in its parameter's memory format (a channels-last model keeps
     channels-last weights; ``channels_last`` is _cl of the parameter as the layer received
@@ -438,6 +492,9 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
     relu_out = False
     input_is_relu = False
     grad_masked_downstream = False
+    # fp32 path: also write y channels-last for a consumer that is itself an fp32 MFMA layer
+    # (DeconvNet sets it): that layer then reads it instead of transposing y
+    cl_twin_out = False
 
     def extra_repr(self):
         fl = [n for n in ("relu_out", "input_is_relu", "grad_masked_downstream") if getattr(self, n)]
@@ -454,8 +511,27 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
                      or (self.out_channels <= 4 and self.in_channels <= 248))
                 and x.shape[0] <= 65535)
 
+    def _mfma_f32_ok(self, x):
+        return (MFMA_DECONV_F32 and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+                and self.weight.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
+                and self.kernel_size == (4, 4) and self.stride == (2, 2) and self.padding == (1, 1)
+                and self.output_padding == (0, 0) and self.dilation == (1, 1) and self.groups == 1
+                and self.in_channels % 4 == 0 and 4 < self.out_channels <= 208)
+
     def forward(self, x, output_size=None):
         F_ = torch.nn.functional
+        if output_size is None and self._mfma_f32_ok(x):
+            from .. import _lib
+            flags = ((_lib.LV_DECONV_RELU_OUT if self.relu_out else 0)
+                     | (_Deconv4s2.SKIP_MASK if self.relu_out and self.grad_masked_downstream else 0))
+            tw = None if self.input_is_relu else getattr(x, "_lv_cl_twin", None)
+            x_cl = tw[0] if tw is not None and tw[1] == x._version else None
+            y = _Deconv4s2F32.apply(F_.relu(x) if self.input_is_relu else x, self.weight, self.bias, flags,
+                                    x_cl, self.cl_twin_out)
+            if self.cl_twin_out:
+                y._lv_cl_twin = (_Deconv4s2F32.last_twin, y._version)
+            _Deconv4s2F32.last_twin = None
+            return y
         bf16 = x.dtype == torch.bfloat16 or (
             torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
         if output_size is not None or not bf16 or not self._mfma_ok(x):
@@ -521,6 +597,43 @@ class _Conv4s2(torch.autograd.Function):
         return gx, _like(gw, ctx.w_cl), gb
 
 
+class _Conv4s2F32(torch.autograd.Function):
+    """y = conv2d(x, w, b, stride 2, padding 1), k = 4, fp32 NCHW: forward and gw / gb by
+    MIOpen (torch), gx by lv_deconv4s2_fwd_f32 (fp32 MFMA; gy read channels-last) -- the
+    encoder's widest layer, whose dgrad MIOpen runs at ~50 TFLOP/s in fp32
+    (profiles/r06_conv_layers_f32.txt)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.conv2d(x, w, b, 2, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _lib
+        x, w = ctx.saved_tensors
+        N, ci, H, W = x.shape
+        co = w.shape[0]
+        need_x, need_w, need_b = ctx.needs_input_grad
+        need_b = need_b and ctx.has_bias
+        gx = gw = gb = None
+        if need_x:
+            st = _lib.stream()
+            wt = torch.empty(_lib.load().lv_deconv4s2_packed_weight_elems_f32(co), device=x.device,
+                             dtype=torch.float32)
+            _lib.call("lv_deconv4s2_pack_weight_f32", w.contiguous().data_ptr(), wt.data_ptr(), co, ci, st)
+            gyc = gy.contiguous(memory_format=torch.channels_last)
+            gx = torch.empty_like(x, memory_format=torch.contiguous_format)
+            _lib.call("lv_deconv4s2_fwd_f32", gyc.data_ptr(), wt.data_ptr(), None, gx.data_ptr(), None,
+                      N, H // 2, W // 2, co, ci, 0, st)
+        if need_w or need_b:
+            _, gw, gb = torch.ops.aten.convolution_backward(
+                gy, x, w, [co] if need_b else None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                [False, need_w, need_b])
+        return gx, gw, gb
+
+
 class MfmaDgradConv2d(nn.Conv2d):
     """nn.Conv2d (same parameters / state_dict) whose k4 s2 p1 input gradient runs on the
     library's MFMA transposed-convolution kernel for bf16 channels-last inputs (autocast
@@ -534,7 +647,19 @@ class MfmaDgradConv2d(nn.Conv2d):
                 and self.out_channels % 8 == 0 and self.in_channels % 4 == 0
                 and self.in_channels <= 208 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
 
+    def _ok_f32(self, x):
+        # fp32: where the kernel's 208-channel tiles are mostly used (c_in > 104: the
+        # 200 -> 400 layer; narrower outputs leave most of its MFMA tiles empty)
+        return (MFMA_DECONV_F32 and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+                and self.weight.dtype == torch.float32 and x.requires_grad
+                and not torch.is_autocast_enabled("cuda") and self.kernel_size == (4, 4)
+                and self.stride == (2, 2) and self.padding == (1, 1) and self.dilation == (1, 1)
+                and self.groups == 1 and self.padding_mode == "zeros" and self.out_channels % 4 == 0
+                and 104 < self.in_channels <= 208 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
+
     def forward(self, x):
+        if self._ok_f32(x):
+            return _Conv4s2F32.apply(x, self.weight, self.bias)
         ac = _autocast_bf16()
         bf16 = x.dtype == torch.bfloat16 or ac
         if not bf16 or not self._ok(x):
@@ -624,6 +749,7 @@ class DeconvNet(nn.Sequential):
                 layers[i + 1] = nn.Identity()
             layers[7].grad_masked_downstream = True
             layers[9].input_is_relu = True
+            layers[3].cl_twin_out = layers[5].cl_twin_out = True  # fp32: layers 3, 4 read them
         super().__init__(*layers)
 
 

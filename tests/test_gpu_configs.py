@@ -938,6 +938,82 @@ def test_mfma_deconv_module_under_autocast(gpu_device):
     torch.testing.assert_close(m.bias.grad, r.bias.grad, rtol=2e-2, atol=2e-2)
 
 
+def F32_ACC_TOL(K):
+    """Max-error allowance (relative to the output's scale) for a K-term fp32 accumulation:
+    sqrt(K) units of 2^-23, the random-walk size of K fp32 roundings with a 2x margin.  Used
+    where the MFMA kernel's sequential K order and MIOpen's blocked order differ (MIOpen can
+    be the more accurate at large K)."""
+    return K ** 0.5 * 2.0 ** -23
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,relu", [(3, 200, 200, 16, 16, 0), (4, 200, 200, 4, 4, 1),
+                                                (2, 16, 8, 5, 3, 0), (5, 64, 200, 7, 9, 1),
+                                                (2, 200, 5, 17, 16, 0), (2, 12, 208, 6, 10, 0),
+                                                (64, 200, 200, 8, 8, 1)])
+def test_mfma_deconv_f32_matches_float64(gpu_device, N, Cin, Cout, H, W, relu):
+    """lv_deconv4s2_fwd_f32 (fp32 operands on v_mfma_f32_16x16x4_f32, NCHW output) against
+    conv_transpose2d(stride 2, padding 1) in float64 on the same fp32 operands.  The bar is
+    the reference's own precision: torch's fp32 layer (MIOpen, what nn.ConvTranspose2d runs
+    in the reference's fp32 training) has some max error e against float64; ours must stay
+    within 2 e (or F32_ACC_TOL(K) of the output's scale), and within 1e-5 normwise.  Ragged pixel
+    tiles, border taps, Cout not a multiple of 16, the fused ReLU; the channels-last twin
+    output bit for bit equal to y."""
+    from lie_vae.experiments.nets import _Deconv4s2F32
+    from lie_vae import _lib
+    g = torch.Generator().manual_seed(N * 1000 + Cin + H + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cin, Cout, 4, 4, generator=g) * 0.05
+    b = torch.randn(Cout, generator=g)
+    ref = torch.nn.functional.conv_transpose2d(x.double(), w.double(), b.double(), 2, 1)
+    xg, wg, bg = x.to(gpu_device), w.to(gpu_device), b.to(gpu_device)
+    yt = torch.nn.functional.conv_transpose2d(xg, wg, bg, 2, 1)
+    if relu:
+        ref, yt = ref.clamp_min(0), yt.clamp_min(0)
+    twin = Cout % 4 == 0
+    y = _Deconv4s2F32.apply(xg, wg, bg, _lib.LV_DECONV_RELU_OUT if relu else 0, None, twin)
+    assert y.shape == ref.shape and y.dtype == torch.float32 and y.is_contiguous()
+    if twin:  # the channels-last copy the epilogue writes beside y (the next layer's input)
+        ycl = _Deconv4s2F32.last_twin
+        assert ycl.is_contiguous(memory_format=torch.channels_last) and torch.equal(ycl, y)
+    yd, ytd = y.double().cpu(), yt.double().cpu()
+    e, e_t = (yd - ref).abs().max().item(), (ytd - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert e <= max(2 * e_t, F32_ACC_TOL(4 * Cin) * scale), (e, e_t, scale)
+    assert (yd - ref).norm() <= 1e-5 * ref.norm(), ((yd - ref).norm() / ref.norm()).item()
+
+
+def test_mfma_deconv_f32_module_matches_plain_layer(gpu_device):
+    """MfmaConvTranspose2d in fp32 (no autocast; nets.MFMA_DECONV_F32) with the fused ReLU:
+    forward within fp32 rounding of nn.ConvTranspose2d + ReLU, gradients (the same
+    convolution_backward, gy masked by the ReLU) likewise; a second layer reading the
+    first's channels-last twin gives the same bits as reading a transposed copy."""
+    from lie_vae.experiments.nets import MfmaConvTranspose2d
+    torch.manual_seed(19)
+    m = MfmaConvTranspose2d(200, 200, 4, 2, 1).to(gpu_device)
+    m.relu_out = True
+    m.cl_twin_out = True
+    m2 = MfmaConvTranspose2d(200, 200, 4, 2, 1).to(gpu_device)
+    with torch.no_grad():
+        y1 = m(torch.randn(4, 200, 4, 4, device=gpu_device))
+        assert y1._lv_cl_twin[0] is not None
+        z_twin = m2(y1)
+        z_copy = m2(y1.clone())
+    assert torch.equal(z_twin, z_copy)
+    m.cl_twin_out = False
+    r = torch.nn.ConvTranspose2d(200, 200, 4, 2, 1).to(gpu_device)
+    r.load_state_dict(m.state_dict())
+    x = torch.randn(16, 200, 8, 8, device=gpu_device)
+    gy = torch.randn(16, 200, 16, 16, device=gpu_device)
+    xs = [x.clone().requires_grad_(True) for _ in range(2)]
+    ym, yr = m(xs[0]), torch.relu(r(xs[1]))
+    torch.testing.assert_close(ym, yr, rtol=1e-5, atol=1e-5)
+    (ym * gy).sum().backward()
+    (yr * gy).sum().backward()
+    torch.testing.assert_close(xs[0].grad, xs[1].grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(m.weight.grad, r.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(m.bias.grad, r.bias.grad, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(3, 200, 3, 32, 32), (2, 40, 1, 9, 21), (2, 200, 4, 17, 16),
                                            (1, 248, 3, 5, 40), (2, 64, 200, 7, 9)])
 def test_mfma_deconv_backward_matches_autograd(gpu_device, N, Cin, Cout, H, W):
@@ -998,6 +1074,33 @@ def test_mfma_conv_dgrad_matches_autograd(gpu_device, N, Cin, Cout, H, W):
         rms = ref.square().mean().sqrt()
         bad = (gd - ref).abs() > rel * ref.abs() + absr * rms
         assert not bad.any(), f"{name}: {int(bad.sum())} of {bad.numel()} off, max err {(gd - ref).abs().max():.3e}"
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(3, 200, 400, 8, 8), (2, 120, 36, 10, 6)])
+def test_mfma_conv_dgrad_f32_matches_float64(gpu_device, N, Cin, Cout, H, W):
+    """The fp32 encoder dgrad (_Conv4s2F32: gx by lv_deconv4s2_fwd_f32 with the Conv2d weight
+    read as a transposed-convolution weight) against float64 autograd of conv2d on the same
+    fp32 x, w and gy: within 2x torch's own fp32 gx error (MIOpen, the reference's layer) or
+    F32_ACC_TOL(K) of the scale, 1e-5 normwise; gw / gb are MIOpen's own (fp32 tolerance)."""
+    from lie_vae.experiments.nets import _Conv4s2F32
+    g = torch.Generator().manual_seed(N * 13 + Cin + H)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 4, 4, generator=g) * 0.05
+    b = torch.randn(Cout, generator=g)
+    gy = torch.randn(N, Cout, H // 2, W // 2, generator=g)
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.conv2d(xr, wr, br, 2, 1).backward(gy.double())
+    xd, wd, bd = (t.to(gpu_device).requires_grad_(True) for t in (x, w, b))
+    _Conv4s2F32.apply(xd, wd, bd).backward(gy.to(gpu_device))
+    xt = x.to(gpu_device).requires_grad_(True)
+    torch.nn.functional.conv2d(xt, w.to(gpu_device), b.to(gpu_device), 2, 1).backward(gy.to(gpu_device))
+    ref = xr.grad
+    e = (xd.grad.double().cpu() - ref).abs().max().item()
+    e_t = (xt.grad.double().cpu() - ref).abs().max().item()
+    assert e <= max(2 * e_t, F32_ACC_TOL(4 * Cout) * ref.abs().max().item()), (e, e_t)
+    assert (xd.grad.double().cpu() - ref).norm() <= 1e-5 * ref.norm()
+    torch.testing.assert_close(wd.grad.double().cpu(), wr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bd.grad.double().cpu(), br.grad, rtol=1e-4, atol=1e-4)
 
 
 def test_small_deconv_mask_gx_bitwise(gpu_device):
