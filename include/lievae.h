@@ -154,13 +154,14 @@ size_t lv_group_action_bwd_workspace(int64_t n, int L, int C, int shared_F);
  * follow the part (a CPX partition has fewer CUs). */
 int lv_compute_units(void);
 
-/* Launch plans (host only, no kernel launch; for tests and capacity planning; the backward
- * reads the device's CU count as lv_compute_units does).  plan[] gets
+/* Launch plans (host only, no kernel launch; for tests and capacity planning; both read the
+ * device's CU count as lv_compute_units does: the forward's waves per block and the
+ * backward's persistent grid follow it).  plan[] gets
  * LV_PLAN_LEN values: [0] forward: tile kernel (1) or grid-stride kernel (0); backward:
  * spectrum mode (0 per-sample, 1 shared in LDS, 2 shared from global memory with the dF
  * slab in the workspace -- the large-tile fallback, 3 the persistent kernel: C = 10,
- * 3 <= l <= 10, shared spectrum, from 3 * CUs + 1 six-sample groups (769 on MI355X),
- * 3 blocks per CU, one dF slab per block), [1] grid blocks,
+ * 3 <= l <= 10, shared spectrum, from CUs + 1 six-sample groups (257 on MI355X), a grid
+ * of min(groups, 3 * CUs) blocks, one dF slab per block), [1] grid blocks,
  * [2] degree segments, [3] threads per block, [4] dynamic LDS bytes per block,
  * [5] samples per block group, [6] forward: write-through stores / backward: workspace
  * bytes, [7..23] segment boundaries seg_lo[0..segments] (then -1), [24..39] the degree

@@ -638,8 +638,11 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
       const int pv = ((p.a.variant & kBwdVarPersistPad) ? 1 : 0) | ((p.a.variant & kBwdVarPersistAng) ? 2 : 0) |
                      ((p.a.variant & kBwdVarPersistBufDma) ? 4 : 0) | ((p.a.variant & kBwdVarPersistLaneMap) ? 8 : 0);
       // built single-buffer variants: 0 (round 5), 2 (LDS angle sums), 3 (+ padded tile),
-      // 6 (+ buffer DMA), 14 (+ lane map); the A/B library refuses other combinations
-      if (single && pv == 14)
+      // 6 (+ buffer DMA), 7 (padded tile by buffer DMA), 14 (+ lane map); the A/B library
+      // refuses other combinations
+      if (single && pv == 7)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 7>), grid, block, p.lds, p.stream, p.a);
+      else if (single && pv == 14)
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 14>), grid, block, p.lds, p.stream, p.a);
       else if (single && pv == 6)
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 6>), grid, block, p.lds, p.stream, p.a);

@@ -108,6 +108,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr bool PAD = (PV & 1) != 0 && persist_pad(LT) > 0;
   constexpr bool ANGL = (PV & 2) != 0;
   constexpr bool BUFDMA = (PV & 4) != 0 && !((PV & 1) != 0 && persist_pad(LT) > 0);
+  constexpr bool PADBUF = (PV & 4) != 0 && PAD;  // padded tile by buffer loads to LDS
   constexpr bool LMAP = (PV & 8) != 0 && ANGL && !((PV & 1) != 0 && persist_pad(LT) > 0) &&
                         ((LT + 1) * (LT + 1) * 10) % 32 == 26;
   constexpr int C = kTileFastC;
@@ -176,6 +177,25 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
       const int head = min((16 - mis) & 15, span);
       const int nvec = (span - head) >> 4;
       const int tail0 = head + nvec * 16;
+      if constexpr (PADBUF) {
+        // the same pieces by buffer loads: the group's bytes as a buffer resource, a piece's
+        // source offset from its LDS offset by one constant division (no 64-bit address)
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(gb), 0, nbytes, kRawBufferFlags);
+        for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
+          if (v0 + lane < nvec) {
+            const int rel = head + 16 * (v0 + lane);
+            const int jp = (rel + 15) / (kStride * 4);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(stage_b + head + 16 * v0), 16, rel - jp * kPadB, 0, 0, 0);
+          }
+        if (wave == NW - 1) {
+          if (4 * lane < head) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(stage_b), 4, 4 * lane, 0, 0, 0);
+          const int tb = tail0 + 4 * lane;
+          if (tb < span)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, as_lds(stage_b + tail0), 4, tb - (Sv - 1) * kPadB, 0, 0, 0);
+        }
+        return;
+      }
       for (int v0 = wave * 64; v0 < nvec; v0 += nthr)
         if (v0 + lane < nvec) {
           // piece at LDS offset rel: the sample holding its last byte, its global bytes

@@ -570,6 +570,54 @@ def test_persistent_backward_other_grid_sizes_vs_oracle(gpu_device, tmp_path):
         assert_grad_parity(r["ga"], ga32, ga64, what=f"gang, {bpc} blocks per CU")
 
 
+_FWD_SEG_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import lie_vae._ops as ops
+dev = torch.device("cuda:0")
+out = {}
+for n in (4097, 16385):
+    g = torch.Generator().manual_seed(n)
+    v = torch.randn(n, 3, generator=g).to(dev)
+    F = torch.randn(121, 10, generator=g).to(dev)
+    out[f"y{n}"] = ops.fused_exp_action(None, v, F, 10).cpu().numpy()
+import lie_vae._lib as lib
+out["seg"] = lib.plan("fwd", 1, 0, lib.LV_DTYPE_F32, 4097, 10, 10)["segments"]
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_forward_wave_counts_and_degree_sets_bitwise(gpu_device, tmp_path):
+    """The forward tile kernel's plan (waves per block by groups per CU, degree sets by the
+    cost model) changes which wave computes which degree, never a degree's arithmetic:
+    every wave count 4-8 and a hand-made degree set (A/B library knobs LV_TILE_NSEG /
+    LV_TILE_MASKS) give the product library's output bit for bit (config-2 shape, a ragged
+    4,097 and 16,385)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "lie-vae_amd")
+    runs = {"product": {}}
+    for k in (4, 5, 6, 7, 8):
+        runs[f"nseg{k}"] = {"LV_TILE_NSEG": str(k)}
+    runs["masks"] = {"LV_TILE_NSEG": "6", "LV_TILE_MASKS": "400:200:102:84:48:31"}
+    res = {}
+    for tag, extra in runs.items():
+        out = str(tmp_path / f"{tag}.npz")
+        # the ctypes path (no liblievae_torch.so, which links the product library), so the
+        # A/B library's kernels are the ones that run
+        env = dict(os.environ, LIEVAE_TORCH_OPS_LIB=str(tmp_path / "none.so"), **extra)
+        if tag != "product":
+            env["LIEVAE_HIP_LIB"] = os.path.join(pkg, "lie_vae", "liblievae_hip_ab.so")
+        subprocess.run([sys.executable, "-c", _FWD_SEG_SCRIPT, pkg, out], env=env, check=True, timeout=180)
+        res[tag] = np.load(out)
+    for k in (4, 5, 6, 7, 8):
+        assert int(res[f"nseg{k}"]["seg"]) == k  # the knob took effect
+    for tag, r in res.items():
+        for key in ("y4097", "y16385"):
+            assert np.array_equal(r[key], res["product"][key]), (tag, key)
+
+
 def test_action_large_tiles_fallback_vs_oracle(gpu_device):
     """Tiles too large for the LDS plans (large C at high l; include/lievae.h plan mode 2):
     the forward's grid-stride kernel and the backward's global-spectrum fallback (dF slab
