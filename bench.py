@@ -23,9 +23,9 @@ Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §6):
                    (fp32 recursion), HBM and fp32-VALU roofline fractions
   train_step       BASELINE config 3 (N = 1: B = 512) / config 4 (N > 1: 512 per rank,
                    RCCL bucketed all-reduce of the gradients): the full VAE training step
-                   (unsupervised.py:108-117) at reference precision (fp32) and with bf16
-                   autocast, samples/s of the whole job, max over ranks, the median of
-                   3 timed rounds (each round's time in the record)
+                   (unsupervised.py:108-117) with bf16 autocast and at reference
+                   precision (fp32; in that order), samples/s of the whole job, max over
+                   ranks, the median of 3 timed rounds (each round's time in the record)
   fwd_bwd.*.roofline_valu  the group-action backward's VALU-issue roofline (it is VALU-bound
                    at large batch): PMC VALU instructions per call at the measured FMA
                    issue rate, as a fraction of the call time
@@ -608,7 +608,9 @@ def bench_train_step(dev, env, steps, warmup):
     torch.backends.cudnn.benchmark = False
     recs = {}
     t0 = time.perf_counter()
-    for tag, amp, cl in (("f32", "off", False), ("bf16", "bf16", True)):
+    # bf16 first: right after the fp32 step's 100 TFLOP/s fp32-MFMA layers its first rounds
+    # ran 20-30% slow (5.46 / 5.33 / 4.37 ms against 3.8-4.0 in steady state)
+    for tag, amp, cl in (("bf16", "bf16", True), ("f32", "off", False)):
         torch.manual_seed(0)
         model = VAE(latent_mode="so3", decoder_mode="action", degrees=10, rep_copies=10,
                     rgb=True, batch_norm=True, deconv_hidden=200, mean_mode="s2s2").to(dev)
