@@ -91,7 +91,7 @@ def parse():
                     help="config-5 record: launches timed per round (0: skip the record)")
     ap.add_argument("--train-steps", type=int, default=10,
                     help="train_step record: timed steps per precision (0: skip the record)")
-    ap.add_argument("--train-warmup", type=int, default=5)
+    ap.add_argument("--train-warmup", type=int, default=10)
     ap.add_argument("--no-ang", action="store_true",
                     help="A/B only: time the instantiation without the angles output")
     ap.add_argument("--dry-run", action="store_true",
@@ -606,6 +606,12 @@ def bench_train_step(dev, env, steps, warmup):
     from lie_vae.experiments.vae import VAE
     db = nets.use_packaged_miopen_db()
     torch.backends.cudnn.benchmark = False
+    # the buffers of the records before (sweep, cold-cache scrub, config 5) back to the
+    # device: the step's allocations then come from fresh segments, as in a training
+    # process (bench_train.py alone: 3.80 ms bf16; after them without this, 4.0-5.8)
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
     recs = {}
     t0 = time.perf_counter()
     # bf16 first: right after the fp32 step's 100 TFLOP/s fp32-MFMA layers its first rounds
