@@ -418,12 +418,12 @@ MFMA_DECONV_F32 = True
 
 class _Deconv4s2F32(torch.autograd.Function):
     """y = conv_transpose2d(x, w, b, stride 2, padding 1), k = 4, fp32 NCHW in and out: the
-    forward on lv_deconv4s2_fwd_f32 (x read channels-last: one transposing copy), with
+    forward on lv_deconv4s2_fwd_f32 (x read channels-last: x_cl if given, else one
+    transposing copy; with twin also y channels-last as the second, non-differentiable
+    output, else an empty tensor there), with
     LV_DECONV_RELU_OUT returning relu(y) (the backward then masks gy by y > 0, unless
     SKIP_MASK: the consumer of y returns a masked gradient).  Backward: gx, gw, gb by
     aten.convolution_backward on the saved fp32 operands, what nn.ConvTranspose2d runs."""
-
-    last_twin = None  # the channels-last twin of the latest forward's y (see MfmaConvTranspose2d)
 
     @staticmethod
     def forward(ctx, x, w, b, flags=0, x_cl=None, twin=False):
@@ -439,7 +439,6 @@ class _Deconv4s2F32(torch.autograd.Function):
         y = torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=torch.float32)
         ycl = (torch.empty((N, Cout, 2 * H, 2 * W), device=x.device, dtype=torch.float32,
                            memory_format=torch.channels_last) if twin else None)
-        _Deconv4s2F32.last_twin = ycl
         _lib.call("lv_deconv4s2_fwd_f32", xc.data_ptr(), wt.data_ptr(), None if b is None else b.data_ptr(),
                   y.data_ptr(), None if ycl is None else ycl.data_ptr(), N, H, W, Cin, Cout,
                   flags & _lib.LV_DECONV_RELU_OUT, st)
@@ -448,10 +447,13 @@ class _Deconv4s2F32(torch.autograd.Function):
         ctx.has_bias = b is not None
         ctx.relu_out = relu_out
         ctx.w_cl = _cl(w)
-        return y
+        if ycl is None:
+            ycl = y.new_empty(0)
+        ctx.mark_non_differentiable(ycl)
+        return y, ycl
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, _gycl):
         x, w = ctx.saved_tensors[:2]
         Cout = w.shape[1]
         if ctx.relu_out:
@@ -526,11 +528,10 @@ class MfmaConvTranspose2d(nn.ConvTranspose2d):
                      | (_Deconv4s2.SKIP_MASK if self.relu_out and self.grad_masked_downstream else 0))
             tw = None if self.input_is_relu else getattr(x, "_lv_cl_twin", None)
             x_cl = tw[0] if tw is not None and tw[1] == x._version else None
-            y = _Deconv4s2F32.apply(F_.relu(x) if self.input_is_relu else x, self.weight, self.bias, flags,
-                                    x_cl, self.cl_twin_out)
+            y, ycl = _Deconv4s2F32.apply(F_.relu(x) if self.input_is_relu else x, self.weight, self.bias,
+                                         flags, x_cl, self.cl_twin_out)
             if self.cl_twin_out:
-                y._lv_cl_twin = (_Deconv4s2F32.last_twin, y._version)
-            _Deconv4s2F32.last_twin = None
+                y._lv_cl_twin = (ycl, y._version)
             return y
         bf16 = x.dtype == torch.bfloat16 or (
             torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)

@@ -970,10 +970,9 @@ def test_mfma_deconv_f32_matches_float64(gpu_device, N, Cin, Cout, H, W, relu):
     if relu:
         ref, yt = ref.clamp_min(0), yt.clamp_min(0)
     twin = Cout % 4 == 0
-    y = _Deconv4s2F32.apply(xg, wg, bg, _lib.LV_DECONV_RELU_OUT if relu else 0, None, twin)
+    y, ycl = _Deconv4s2F32.apply(xg, wg, bg, _lib.LV_DECONV_RELU_OUT if relu else 0, None, twin)
     assert y.shape == ref.shape and y.dtype == torch.float32 and y.is_contiguous()
     if twin:  # the channels-last copy the epilogue writes beside y (the next layer's input)
-        ycl = _Deconv4s2F32.last_twin
         assert ycl.is_contiguous(memory_format=torch.channels_last) and torch.equal(ycl, y)
     yd, ytd = y.double().cpu(), yt.double().cpu()
     e, e_t = (yd - ref).abs().max().item(), (ytd - ref).abs().max().item()
