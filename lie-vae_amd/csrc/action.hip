@@ -681,9 +681,12 @@ constexpr int kBwdReduceDefault = 6;
 // -> 358, 16,384 31.9 -> 30.6; the padded tile, kBwdVarPersistPad, was slower alone and
 // with it: 104.5 / 100.2-100.9 us, profiles/r06_ab_persist.txt), and its gradient tile
 // by buffer loads to LDS with SGPR round offsets (65,536 99.2-100.5 -> 96.8-97.5 us,
-// 4,096 13.7-13.9 -> 13.3-13.5, 262,144 359-360 -> 351-352; profiles/r06_ab_bufdma.txt)
-constexpr int kBwdVariantDefault =
-    kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1 | kBwdVarPersistAng | kBwdVarPersistBufDma;
+// 4,096 13.7-13.9 -> 13.3-13.5, 262,144 359-360 -> 351-352; profiles/r06_ab_bufdma.txt),
+// and its dF slab as 16-byte write-through stores (4,096 13.47-13.52 -> 12.92-13.03 us,
+// 16,384 29.9-30.3 -> 29.4-29.5, 2,048 10.4 -> 10.25, 65,536 unchanged; dF bitwise equal;
+// profiles/r06_ab_slabwt.txt)
+constexpr int kBwdVariantDefault = kBwdVarJit | kBwdVarPersistSingle | kBwdVarPersistTask1 | kBwdVarPersistAng |
+                                   kBwdVarPersistBufDma | kBwdVarPersistSlabWT;
 
 // Fallback for tiles that leave no LDS room for the spectrum and the dF slab (large C at
 // high l): the whole CU's LDS, the spectrum read from global memory and the slab kept in

@@ -636,11 +636,14 @@ int BwdLauncher<LT>::run(BwdLaunch& p) {
     if constexpr (LT <= kBwdPersistMaxL) {
       const bool single = (p.a.variant & kBwdVarPersistSingle) != 0;
       const int pv = ((p.a.variant & kBwdVarPersistPad) ? 1 : 0) | ((p.a.variant & kBwdVarPersistAng) ? 2 : 0) |
-                     ((p.a.variant & kBwdVarPersistBufDma) ? 4 : 0) | ((p.a.variant & kBwdVarPersistLaneMap) ? 8 : 0);
+                     ((p.a.variant & kBwdVarPersistBufDma) ? 4 : 0) | ((p.a.variant & kBwdVarPersistLaneMap) ? 8 : 0) |
+                     ((p.a.variant & kBwdVarPersistSlabWT) ? 16 : 0);
       // built single-buffer variants: 0 (round 5), 2 (LDS angle sums), 3 (+ padded tile),
-      // 6 (+ buffer DMA), 7 (padded tile by buffer DMA), 14 (+ lane map); the A/B library
-      // refuses other combinations
-      if (single && pv == 7)
+      // 6 (+ buffer DMA), 7 (padded tile by buffer DMA), 14 (+ lane map), 22 (6 + write-through
+      // slab stores); the A/B library refuses other combinations
+      if (single && pv == 22)
+        hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 22>), grid, block, p.lds, p.stream, p.a);
+      else if (single && pv == 7)
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 7>), grid, block, p.lds, p.stream, p.a);
       else if (single && pv == 14)
         hipLaunchKernelGGL((action_bwd_persist_kernel<LT, kBwdPersistWaves, false, true, 3, 14>), grid, block, p.lds, p.stream, p.a);

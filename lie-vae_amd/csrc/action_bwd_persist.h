@@ -65,6 +65,10 @@ constexpr int kBwdVarPersistBufDma = 4096;
 // that: 1 extra LDS cycle per tile access instead of 2.  Entries are 16 j + c; lanes 60-63
 // are idle (j = 6).  Used where M*C = 26 mod 32 (l = 4, 10).
 constexpr int kBwdVarPersistLaneMap = 8192;
+// kBwdVarPersistSlabWT: the block's dF slab leaves as whole 16-byte pieces with write-through
+// (sc1) buffer stores after one block barrier, instead of each wave's rows as 4-byte stores
+// left dirty in the XCD's L2 for the end-of-kernel write-back.
+constexpr int kBwdVarPersistSlabWT = 16384;
 static __constant__ unsigned char kPersistLaneJC[64] = {
     0, 1, 2, 3, 5, 6, 7, 8, 9, 17, 18, 19, 21, 24, 32, 34, 37, 38, 49, 52, 53, 55,
     57, 66, 70, 72, 73, 81, 82, 86, 87, 89, 4, 16, 20, 22, 23, 25, 33, 35, 36, 39,
@@ -109,6 +113,7 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
   constexpr bool ANGL = (PV & 2) != 0;
   constexpr bool BUFDMA = (PV & 4) != 0 && !((PV & 1) != 0 && persist_pad(LT) > 0);
   constexpr bool PADBUF = (PV & 4) != 0 && PAD;  // padded tile by buffer loads to LDS
+  constexpr bool SLABWT = (PV & 16) != 0;
   constexpr bool LMAP = (PV & 8) != 0 && ANGL && !((PV & 1) != 0 && persist_pad(LT) > 0) &&
                         ((LT + 1) * (LT + 1) * 10) % 32 == 26;
   constexpr int C = kTileFastC;
@@ -505,6 +510,22 @@ void action_bwd_persist_kernel(ActionBwdArgs a) {
     }
   }
   // ---- the block's slab (each wave its own rows) to the workspace, chunk-major
+  if constexpr (SLABWT) {
+    block_sync_lds();  // every wave's slab rows are final
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int nch = (MC + kSlabChunk - 1) / kSlabChunk;
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(a.ws_F, 0, nch * (int)gridDim.x * kSlabChunk * 4, kRawBufferFlags);
+    // piece (chunk q, quarter k): slab[16 q + 4 k ..] -> ws_F[q * grid * 16 + block * 16 + 4 k ..]
+    // (the last chunk's pad reads the next LDS floats: summed by reduce5, never stored to gF)
+    for (int pc = tid; pc < 4 * nch; pc += nthr) {
+      const int q = pc >> 2, k = pc & 3;
+      const f4 v = *reinterpret_cast<const f4*>(slab + kSlabChunk * q + 4 * k);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rw, ((q * (int)gridDim.x + (int)blockIdx.x) * kSlabChunk + 4 * k) * 4,
+                                             0, 16);
+    }
+    return;
+  }
   for (unsigned m = dmask; m; m &= m - 1) {
     const int l = __builtin_ctz(m);
     const int g0 = l * l * C, cnt = (2 * l + 1) * C;
