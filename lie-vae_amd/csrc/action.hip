@@ -391,7 +391,9 @@ constexpr double kTileSegCostMid = 260.0;    // -> 8
 constexpr double kTileSegCostLarge = 560.0;  // -> 4
 constexpr int64_t kTileFewGroupsPerCU = 4, kTileMidGroupsPerCU = 16;
 constexpr double kTilePrologue = 60.0;       // per-wave fixed cost: spectrum slice, multiples reads
-constexpr int64_t kWriteThroughMaxBytes = 24ll << 20;
+// round 6 (7 / 8 waves per block): write-through still wins at 6,144 samples (29.7 MB:
+// 8.7-8.8 vs 9.0-9.1 us) and loses from 8,192 (39.6 MB: 11.7 vs 11.4; profiles/r06_ab_wt.txt)
+constexpr int64_t kWriteThroughMaxBytes = 32ll << 20;
 
 // A/B knobs (LV_TILE=0 disables the tile kernel, LV_TILE_WT=0/1 forces the store policy,
 // LV_*_NSEG force segment counts, LV_BWD_FGLOBAL forces the backward's global-spectrum

@@ -110,7 +110,9 @@ def test_pinned_plans_of_the_benchmark_configs():
     # (6*1210*4 + 16 tile + 6*76*4 trig = 30,880 B -> 5 blocks per CU), write-through
     p = _lib.plan("fwd", 1, 0, F32, 4096, 10, 10)
     assert (p["tile"], p["blocks"], p["lds_bytes"], p["aux"]) == (1, 683, 30880, 1)
-    assert _lib.plan("fwd", 1, 0, F32, 65536, 10, 10)["aux"] == 0  # > 24 MB: nt stores
+    assert _lib.plan("fwd", 1, 0, F32, 65536, 10, 10)["aux"] == 0  # > 32 MB: nt stores
+    assert _lib.plan("fwd", 1, 0, F32, 6144, 10, 10)["aux"] == 1   # 29.7 MB: write-through
+    assert _lib.plan("fwd", 1, 0, F32, 8192, 10, 10)["aux"] == 0
     # waves per block by sample groups per CU (profiles/r06_ab_nseg_sweep.txt): 7 up to 4
     # groups per CU, 8 up to 16, 4 beyond
     for n, waves in ((4096, 7), (4 * 6 * CUS, 7), (4 * 6 * CUS + 6, 8), (16384, 8),
