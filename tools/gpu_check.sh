@@ -1,4 +1,4 @@
-# Final round-6 check at HEAD: the GPU test suite, smoke(), the driver-form bench line.
+# Check at HEAD: the GPU test suite, smoke(), the default bench line (gpurun_out/fin2_*.log).
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
