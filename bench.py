@@ -55,8 +55,8 @@ F32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 via v_pk_fma_f32 (= fp
 # tools/valu_rate.hip, profiles/r05_valu_rate.txt), as a fraction of the call time.
 VALU_WAVE_INSTS_PER_NS = 661.19
 BWD_VALU_PER_CALL = {  # batch -> (SQ_INSTS_VALU per call, evidence)
-    4096: (3036250 + 51604, "profiles/r06_pmc_bwd_only_4096.txt"),
-    65536: (40875872 + 51604, "profiles/r06_pmc_persist_65536.txt"),
+    4096: (2911261 + 51604, "profiles/r06_final_pmc_bwd_only_4096.txt"),
+    65536: (40735328 + 51604, "profiles/r06_final_pmc_bwd_only_65536.txt"),
 }
 SCRUB_BYTES = 512 << 20  # > 256 MiB Infinity Cache (MI355X_MICROARCH.md:40)
 
