@@ -171,7 +171,7 @@ def time_train_steps(model, dev, world, rank, global_batch, steps, warmup, amp="
     run = trainer.capture(x) if graph else (lambda: trainer.step(x))
     torch.cuda.synchronize(dev)
     warm_s = time.perf_counter() - t_setup
-    els = []
+    els, issue = [], []
     for _ in range(max(1, rounds)):
         if world > 1:
             dist.barrier()
@@ -179,6 +179,7 @@ def time_train_steps(model, dev, world, rank, global_batch, steps, warmup, amp="
         t0 = time.perf_counter()
         for _ in range(steps):
             loss, recon, kl = run()
+        issue.append(time.perf_counter() - t0)  # host time to issue the steps
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -193,6 +194,8 @@ def time_train_steps(model, dev, world, rank, global_batch, steps, warmup, amp="
         "ranks_seen": nranks, "max_over_ranks": world > 1,
         "steps": steps, "warmup": warmup, "ms_per_step": el * 1e3 / steps,
         "rounds": max(1, rounds), "ms_per_step_rounds": [e * 1e3 / steps for e in els],
+        # host time to issue a round's steps (rank 0): close to the round's time = host-bound
+        "host_issue_ms_per_step_rounds": [e * 1e3 / steps for e in issue],
         "warmup_s": warm_s,
         "config": {"global_batch": global_batch, "per_gpu": B, "params": param_count(model),
                    "dtype": "f32" if amp == "off" else "bf16 autocast (convs/linear), f32 SO(3)",
