@@ -83,6 +83,22 @@ for s in "$@"; do
         timeout -k 10 300 python bench_train.py --steps 30 --warmup 10 --no-find "$@" > "gpurun_out/tg_$tag.log" 2>&1 || exit 1
         echo "$tag $(grep '^{' "gpurun_out/tg_$tag.log" | tail -1)" >> gpurun_out/ab_train_graph.log
       done; cat gpurun_out/ab_train_graph.log ;;
+    # the train-step record's rounds and host issue time: bench.py twice, bench_train.py alone
+    train_diag)
+      for i in 1 2; do
+        timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "gpurun_out/trd_$i.log" 2>&1 || exit 1
+        tail -n 1 "gpurun_out/trd_$i.log" >> gpurun_out/train_diag.log
+      done
+      timeout -k 10 300 python bench_train.py --steps 30 --warmup 10 --no-find --amp bf16 --channels-last \
+        | grep "^{" >> gpurun_out/train_diag.log || exit 1 ;;
+    # MIOpen immediate mode (the record's) against find mode (torch caches the picked solver)
+    train_find)
+      for cfg in "bf16_nofind --amp bf16 --channels-last --no-find" "bf16_find --amp bf16 --channels-last" \
+                 "f32_nofind --amp off --no-find" "f32_find --amp off"; do
+        set -- $cfg; tag=$1; shift
+        timeout -k 10 500 python bench_train.py --steps 30 --warmup 10 "$@" > "gpurun_out/tf_$tag.log" 2>&1 || exit 1
+        echo "$tag $(grep '^{' "gpurun_out/tf_$tag.log" | tail -1)" >> gpurun_out/train_find.log
+      done; cat gpurun_out/train_find.log ;;
     # in-kernel phase timeline of the config-2 forward (LV_STAMPS)
     timeline) LIEVAE_HIP_LIB=$AB LV_STAMPS=1 timeout -k 10 120 python tools/timeline.py 4096 10 f32 fwd > gpurun_out/timeline_fwd.log 2>&1; cat gpurun_out/timeline_fwd.log ;;
     *) echo "unknown section $s"; exit 2 ;;
