@@ -32,7 +32,8 @@ def timed(fn, n=10):
     return e0.elapsed_time(e1) * 1e3 / n
 
 
-for H in (4, 8, 16):
+# argv[1] (optional): one input size only, e.g. 16 for the 16 -> 32 layer (PMC runs)
+for H in ((int(sys.argv[1]),) if len(sys.argv) > 1 else (4, 8, 16)):
     Cin = Cout = 200
     g = torch.Generator(device=dev).manual_seed(H)
     x = torch.randn(B, Cin, H, H, device=dev, generator=g)
