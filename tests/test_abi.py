@@ -157,3 +157,25 @@ def test_require_device_refuses_cpu():
     from lie_vae import _lib
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.require_device(None, torch.randn(2))
+
+
+def test_deconv_f32_argument_checks_before_any_launch():
+    """lv_deconv4s2_pack_weight_f32 / lv_deconv4s2_fwd_f32 refuse shapes outside the fp32
+    kernel's contract (Cin % 4 == 0, 1 <= Cout <= 208, a channels-last twin only with
+    Cout % 4 == 0) with LV_ERR_ARG and a message, before touching the device; an empty
+    batch is a no-op (LV_OK)."""
+    import ctypes
+    from lie_vae import _lib
+    lib = _lib.load()
+    P = ctypes.c_void_p(16)  # never dereferenced: the checks run first
+    fwd = lib.lv_deconv4s2_fwd_f32
+    assert lib.lv_deconv4s2_packed_weight_elems_f32(200) == 4 * 208 * 4 * 200 + 16
+    assert lib.lv_deconv4s2_pack_weight_f32(P, P, 6, 200, None) == -1
+    assert b"multiple of 4" in lib.lv_last_error()
+    assert lib.lv_deconv4s2_pack_weight_f32(P, P, 200, 209, None) == -1
+    assert fwd(P, P, None, P, None, 2, 4, 4, 6, 200, 0, None) == -1
+    assert fwd(P, P, None, P, None, 2, 4, 4, 200, 209, 0, None) == -1
+    assert fwd(P, P, None, P, P, 2, 4, 4, 200, 6, 0, None) == -1  # twin needs Cout % 4 == 0
+    assert b"twin" in lib.lv_last_error()
+    assert fwd(P, P, None, P, None, 2, 4, 4, 200, 200, 2, None) == -1  # unknown flag
+    assert fwd(P, P, None, P, None, 0, 4, 4, 200, 200, 0, None) == 0   # empty batch
