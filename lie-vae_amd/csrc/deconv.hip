@@ -277,7 +277,7 @@ __device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n wave-
 // XCD: 1-D grid whose consecutive block ids are dealt round-robin over the 8 XCDs; the four
 // phases of a pixel tile get ids b, b + 8, b + 16, b + 24, i.e. the same XCD at about the
 // same time, so the tile's input pixels come from HBM into that XCD's L2 once, not 4 times.
-template <int S, bool XCD, int BM = 256>
+template <int S, bool XCD, int BM = 256, bool RM = false>
 __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
   using T = DeconvV2<S, BM>;
   constexpr int kV2BM = BM, kV2NW = T::kNW;
@@ -285,7 +285,8 @@ __global__ __launch_bounds__(512) void deconv_mfma2_kernel(DeconvArgs a) {
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / T::kWN, wn = wave % T::kWN;
+  // RM: SIMD-balanced wave tiling, as in deconv_mfma_f32_kernel
+  const int wm = RM ? wave % T::kWM : wave / T::kWN, wn = RM ? wave / T::kWM : wave % T::kWN;
   const int t0 = wn * kNT / T::kWN, ntw = (wn + 1) * kNT / T::kWN - t0;  // this wave's channel tiles
   int p, tile;
   if constexpr (XCD) {
@@ -496,14 +497,18 @@ struct DeconvF32Args {
   int relu;
 };
 
-template <int BM, int S>
+template <int BM, int S, bool RM = false>
 __global__ __launch_bounds__(512) void deconv_mfma_f32_kernel(DeconvF32Args a) {
   using T = DeconvF32<BM, S>;
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / T::kWN, wn = wave % T::kWN;
+  // RM: wave w -> (wm, wn) = (w % kWM, w / kWM).  A block's waves go round-robin to the
+  // CU's 4 SIMDs (SIMD = w % 4), and the 13 channel tiles split 3 | 3 | 3 | 4 over wn: with
+  // wn = w % 4 one SIMD holds both 4-tile waves (8 tile-units against 6), with RM the SIMDs
+  // hold 6 / 6 / 7 / 7 -- the block's per-step barrier waits for the busiest SIMD
+  const int wm = RM ? wave % T::kWM : wave / T::kWN, wn = RM ? wave / T::kWM : wave % T::kWN;
   const int t0 = wn * kNT / T::kWN, ntw = (wn + 1) * kNT / T::kWN - t0;
   // XCD-grouped 1-D grid (deconv_mfma2_kernel): phases of a tile on one XCD
   const int bid = (int)blockIdx.x, slot = bid >> 3;
@@ -1219,7 +1224,10 @@ using namespace lv;
 // 256-row tiles' 38 / 74 / 284 and v1's 43 / 88 / 344, all bitwise equal
 // (profiles/r03_deconv_v2.txt).
 constexpr int kDeconvAutoBM = 6;
-constexpr int kDeconvF32Default = 1;
+// fp32 default: 128-row tiles, 2-stage ring, SIMD-balanced wave tiling (variant 5): 16 -> 32
+// 1,684-1,693 -> 1,600-1,607 us, 8 -> 16 463-471 -> 451-453, 4 -> 8 144 -> 132-134
+// (profiles/r06_ab_deconv_f32_rm.txt); the same remap is neutral on the bf16 kernel (bm = 8)
+constexpr int kDeconvF32Default = 5;
 #ifdef LV_AB_KNOBS
 int deconv_env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -1231,21 +1239,21 @@ int deconv_env_int(const char* name, int dflt) {
 #endif
 
 namespace {
-template <int S, bool XCD, int BM = 256>
+template <int S, bool XCD, int BM = 256, bool RM = false>
 int launch_deconv_v2(const DeconvArgs& a, hipStream_t st) {
   const int64_t tiles = (a.M + BM - 1) / BM;
   if constexpr (XCD)
-    hipLaunchKernelGGL((deconv_mfma2_kernel<S, true, BM>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
+    hipLaunchKernelGGL((deconv_mfma2_kernel<S, true, BM, RM>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
                        (DeconvV2<S, BM>::kLds), st, a);
   else
     hipLaunchKernelGGL((deconv_mfma2_kernel<S, false, BM>), dim3((unsigned)tiles, 4), dim3(512),
                        (DeconvV2<S, BM>::kLds), st, a);
   LV_RETURN_LAUNCH("deconv_mfma2_kernel");
 }
-template <int BM, int S>
+template <int BM, int S, bool RM = false>
 int launch_deconv_f32(const DeconvF32Args& a, hipStream_t st) {
   const int64_t tiles = (a.M + BM - 1) / BM;
-  hipLaunchKernelGGL((deconv_mfma_f32_kernel<BM, S>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
+  hipLaunchKernelGGL((deconv_mfma_f32_kernel<BM, S, RM>), dim3((unsigned)(4 * ((tiles + 7) / 8 * 8))), dim3(512),
                      (DeconvF32<BM, S>::kLds), st, a);
   LV_RETURN_LAUNCH("deconv_mfma_f32_kernel");
 }
@@ -1293,24 +1301,26 @@ static int deconv_fwd(const void* x, const void* wt, const float* bias, void* y,
   LV_CHECK_ARG(x && wt && y, "null pointer");
   const int64_t M = N * H * W;
   LV_CHECK_ARG((M + 127) / 128 <= 0x7fffffff, "batch too large");
-  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256 || (bm >= 2 && bm <= 7),
+  LV_CHECK_ARG(bm == 0 || bm == 128 || bm == 256 || (bm >= 2 && bm <= 8),
                "variant must be 0 (auto), 128 / 256 (v1 tile rows) or 2 / 3 (v2 stages), 4 / 5 (+ XCD order)");
   DeconvArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)wt, bias, (__hip_bfloat16*)y, M, H, W, Cin, Cout,
                (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
   if (bm == 0) bm = kDeconvAutoBM;
-  LV_CHECK_ARG(Cout % 8 == 0 || (bm >= 2 && bm <= 7), "the v1 kernels need Cout %% 8 == 0 (got %d)", Cout);
+  LV_CHECK_ARG(Cout % 8 == 0 || (bm >= 2 && bm <= 8), "the v1 kernels need Cout %% 8 == 0 (got %d)", Cout);
   if (bm == 2) return launch_deconv_v2<2, false>(a, (hipStream_t)stream);
   if (bm == 3) return launch_deconv_v2<3, false>(a, (hipStream_t)stream);
   if (bm == 4) return launch_deconv_v2<2, true>(a, (hipStream_t)stream);
   if (bm == 5) return launch_deconv_v2<3, true>(a, (hipStream_t)stream);
   if (bm == 6) return launch_deconv_v2<2, true, 128>(a, (hipStream_t)stream);
   if (bm == 7) return launch_deconv_v2<3, true, 128>(a, (hipStream_t)stream);
+  if (bm == 8) return launch_deconv_v2<2, true, 128, true>(a, (hipStream_t)stream);
   return bm == 256 ? launch_deconv<256>(a, (hipStream_t)stream) : launch_deconv<128>(a, (hipStream_t)stream);
 }
 #ifdef LV_AB_KNOBS
 // bm: 0 = the default, 128 / 256 = v1 (register-staged double buffer) with that pixel-tile
 // height, 2 / 3 = v2 (LDS-DMA ring of that many stages, 4 x 2 wave tiling), 4 / 5 = v2 with
-// 2 / 3 stages and XCD-grouped phases, 6 / 7 = the same with 128-row block tiles
+// 2 / 3 stages and XCD-grouped phases, 6 / 7 = the same with 128-row block tiles, 8 = 6 with
+// SIMD-balanced wave tiling
 int lv_deconv4s2_fwd_bf16_tile(const void* x, const void* wt, const float* bias, void* y, int64_t N,
                                int H, int W, int Cin, int Cout, int bm, void* stream) {
   return deconv_fwd(x, wt, bias, y, N, H, W, Cin, Cout, bm, 0, stream);
@@ -1348,12 +1358,14 @@ int lv_deconv4s2_fwd_f32(const float* x, const float* wt, const float* bias, flo
   LV_CHECK_ARG(N * Cout * 4 * H * W < (1ll << 40) && (M + 127) / 128 * 4 + 32 <= 0x7fffffff, "batch too large");
   DeconvF32Args a{x, wt, bias, y, y_cl, M, H, W, Cin, Cout, (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
   // A/B build: LV_DECONV_F32_VARIANT 1 = 128-row tiles, 2-stage ring (the default); 2 = 3
-  // stages; 3 = 256-row tiles, 2 stages; 4 = 256 rows, 3 stages
+  // stages; 3 = 256-row tiles, 2 stages; 4 = 256 rows, 3 stages; 5 = 1 with SIMD-balanced
+  // wave tiling (RM)
   static const int kVar = LV_DECONV_KNOB("LV_DECONV_F32_VARIANT", kDeconvF32Default);
   switch (kVar) {
     case 2: return launch_deconv_f32<128, 3>(a, (hipStream_t)stream);
     case 3: return launch_deconv_f32<256, 2>(a, (hipStream_t)stream);
     case 4: return launch_deconv_f32<256, 3>(a, (hipStream_t)stream);
+    case 5: return launch_deconv_f32<128, 2, true>(a, (hipStream_t)stream);
     default: return launch_deconv_f32<128, 2>(a, (hipStream_t)stream);
   }
 }

@@ -36,7 +36,8 @@ for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16), (512, 3, 32)]:
                  ("v2_s2", lambda: kern(2)), ("v2_s3", lambda: kern(3)),
                  ("v2_s2_xcd", lambda: kern(4)), ("v2_s3_xcd", lambda: kern(5)),
                  ("v2_128_s2_xcd", lambda: kern(6)), ("v2_128_s3_xcd", lambda: kern(7)),
-                 ("v2_s2_xcd_b", lambda: kern(4))]
+                 ("v2_128_s2_xcd_rm", lambda: kern(8)), ("v2_128_s2_xcd_b", lambda: kern(6)),
+                 ("v2_128_s2_xcd_rm_b", lambda: kern(8))]
     for tag, fn in runs:
         for _ in range(5):
             fn()
@@ -53,7 +54,7 @@ for (N, C, H) in [(512, 200, 4), (512, 200, 8), (512, 200, 16), (512, 3, 32)]:
     if big:  # v2 (both ring depths) against v1: the same MFMA sequence per element
         kern(256)
         y1 = yk.clone()
-        for v in (2, 3, 4, 5, 6, 7):
+        for v in (2, 3, 4, 5, 6, 7, 8):
             yk.fill_(float("nan"))
             kern(v)
             row[f"v2_{v}_bitwise_vs_v1"] = bool(torch.equal(yk, y1))
