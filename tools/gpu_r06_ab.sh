@@ -50,6 +50,9 @@ for s in "$@"; do
                 plan2= ns6b=LV_TILE_NSEG=6 ;;
     nseg_c5) fwd ab_nseg_c5 "$C5 --sweep=" plan= ns6=LV_TILE_NSEG=6 ns7=LV_TILE_NSEG=7 ns5=LV_TILE_NSEG=5 plan2= \
                 ns7b=LV_TILE_NSEG=7 ;;
+    # forward 7-wave degree sets in SIMD-balanced wave order (waves w, w + 4 share a SIMD)
+    simd_c2) fwd ab_simd_c2 "$C2 --sweep=512,2048" plan= simd=LV_TILE_MASKS=200:100:81:400:18:42:24 plan2= \
+                simd2=LV_TILE_MASKS=200:100:81:400:18:42:24 ;;
     # forward store policy, wave priorities, prologue spread; write-through beyond 24 MB
     fwd_knobs) fwd ab_fwd_knobs "$C2 --sweep=8192,16384" plan= wt0=LV_TILE_WT=0 prio0=LV_TILE_PRIO=0 \
                 prio1=LV_TILE_PRIO=1 prio3=LV_TILE_PRIO=3 spread=LV_TILE_SPREAD=1 plan2= ;;
