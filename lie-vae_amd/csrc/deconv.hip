@@ -1359,13 +1359,14 @@ int lv_deconv4s2_fwd_f32(const float* x, const float* wt, const float* bias, flo
   DeconvF32Args a{x, wt, bias, y, y_cl, M, H, W, Cin, Cout, (flags & LV_DECONV_RELU_OUT) ? 1 : 0};
   // A/B build: LV_DECONV_F32_VARIANT 1 = 128-row tiles, 2-stage ring (the default); 2 = 3
   // stages; 3 = 256-row tiles, 2 stages; 4 = 256 rows, 3 stages; 5 = 1 with SIMD-balanced
-  // wave tiling (RM)
+  // wave tiling (RM, the default); 6 = 3 with RM
   static const int kVar = LV_DECONV_KNOB("LV_DECONV_F32_VARIANT", kDeconvF32Default);
   switch (kVar) {
     case 2: return launch_deconv_f32<128, 3>(a, (hipStream_t)stream);
     case 3: return launch_deconv_f32<256, 2>(a, (hipStream_t)stream);
     case 4: return launch_deconv_f32<256, 3>(a, (hipStream_t)stream);
     case 5: return launch_deconv_f32<128, 2, true>(a, (hipStream_t)stream);
+    case 6: return launch_deconv_f32<256, 2, true>(a, (hipStream_t)stream);
     default: return launch_deconv_f32<128, 2>(a, (hipStream_t)stream);
   }
 }

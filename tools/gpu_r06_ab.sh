@@ -70,7 +70,7 @@ for s in "$@"; do
               && LIEVAE_HIP_LIB=$AB LV_BWD_VARIANT=7713 timeout -k 10 600 bash tools/gpu_pmc_bwd_only.sh 65536 action_bwd_persist ;;
     slabwt) bwd ab_slabwt "LV_BWD_VARIANT=6689,LV_BWD_VARIANT=23073,LV_BWD_VARIANT=6689,LV_BWD_VARIANT=23073" 4096 65536 16384 2048 && bwd_tests 23073 ;;
     # fp32 MFMA deconv (LV_DECONV_F32_VARIANT 1 = 128-row tiles, 2 stages; 2 = 3 stages; 3 = 256
-    # rows; 4 = 256 rows, 3 stages; 5 = 1 with SIMD-balanced wave tiling): parity tests and
+    # rows; 4 = 256 rows, 3 stages; 5 = 1 with SIMD-balanced wave tiling, 6 = 3 with it): parity tests and
     # per-layer timing for each (DCF32_VARIANTS overrides the list)
     deconv_f32)
       for v in ${DCF32_VARIANTS:-1 2 3 4 5}; do
